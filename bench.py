@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark of the CG hot path (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A "step" is one CG iteration (loop body of CG::solve, src/CG.hpp:359-436):
+SpMV + p.Ap, r-update + r.r, x/p-update, on synthetic 3-D 7-point Dirichlet
+Poisson CSR (fp64 values, int32 indices, b_i = i + 1, x0 = 0).
+
+* N = 1: the 256^3 grid (the metric's headline config) on one GPU.
+* N > 1 (launched with torch.distributed.run, one rank per GPU): weak
+  scaling — every rank owns a 256^3 z-slab of a 256 x 256 x (256 N) grid;
+  halo exchange of p and the two dot all-reduces go over RCCL.
+
+value = algorithmic HBM bytes of one iteration over the whole job
+(B_alg = 12 nnz + 4 (N+1) + 80 N) x iterations/s, in GB/s.
+Inputs are generated directly in HBM before the timed region.
+
+rank 0 also prints the dominant kernel's roofline (k_spmv_dot, timed with HIP
+events on the solver stream inside the timed region) and, at N = 1, a CPU
+baseline: the oracle's OpenMP restatement of the reference's iteration
+(oracle/cg_oracle.c) timed on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (before libcgx: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import conjugategradient_amd as cga  # noqa: E402
+from conjugategradient_amd._native import F64, check, lib  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+
+
+def b_alg(n: int, nnz: int) -> int:
+    """Algorithmic bytes of one fused CG iteration."""
+    return 12 * nnz + 4 * (n + 1) + 80 * n
+
+
+def spmv_dot_bytes(n: int, nnz: int) -> int:
+    """k_spmv_dot per launch: val 8 + col 4 per entry, rowptr 4 per row,
+    p read once 8 per row, Ap written 8 per row."""
+    return 12 * nnz + 4 * (n + 1) + 16 * n
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--grid", type=int, default=256, help="n of the n^3 grid per GPU")
+    ap.add_argument("--poll", type=int, default=64, help="iterations per host poll")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="time the steps without per-kernel HIP events")
+    return ap.parse_args()
+
+
+def cpu_baseline(n3: int, threads: int, budget_s: float):
+    """The oracle's OpenMP restatement of the reference iteration on a sample
+    of the same workload (same matrix, same b), timed on host cores."""
+    from oracle import oracle as O
+
+    rp, cl, vl = O.poisson(3, n3, n3, n3)
+    n, nnz = len(rp) - 1, len(vl)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    t1, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, 1, threads)  # probe one iteration
+    iters = max(1, min(200, int(budget_s / max(t1, 1e-6))))
+    t, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, iters, threads)
+    its = iters / t
+    return {
+        "value": round(b_alg(n, nnz) * its / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n3}^3 7-pt Poisson, {iters} iterations of the reference command "
+                  f"sequence (oracle/cg_oracle.c orc_cg_fixed_iters_omp, OpenMP), "
+                  f"{its:.3f} it/s, {t:.2f} s",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    L = lib()
+    q = cga.Queue(local)
+    n3 = args.grid
+    nz_global = n3 * world
+    n_local = n3 * n3 * n3
+    row_begin = rank * n_local
+    n_global = n_local * world
+
+    # ---- RCCL communicator (N > 1) ---------------------------------------
+    if world > 1:
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            check(L.cgx_nccl_unique_id(uid, 128))
+        obj = [bytes(uid.raw) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        check(L.cgx_dist_init(q.handle, rank, world, obj[0], 128))
+
+    # ---- inputs generated in HBM -------------------------------------------
+    nnz_local = L.cgx_poisson_nnz(3, n3, n3, nz_global, row_begin, row_begin + n_local)
+    nnz_global = L.cgx_poisson_nnz(3, n3, n3, nz_global, 0, n_global)
+    rows = cga.DeviceArray(q, n_local + 1, np.int32)
+    cols = cga.DeviceArray(q, nnz_local, np.int32)
+    vals = cga.DeviceArray(q, nnz_local, np.float64)
+    check(L.cgx_poisson_fill(q.handle, F64, 3, n3, n3, nz_global, row_begin,
+                             row_begin + n_local, rows.ptr, cols.ptr, vals.ptr))
+    b = cga.DeviceArray(q, n_local, np.float64)
+    x = cga.DeviceArray(q, n_local, np.float64)
+    check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(row_begin)))
+    x.fill(0.0)
+    A = C.c_void_p()
+    if world > 1:
+        check(L.cgx_csr_create_dist(q.handle, n_global, row_begin, n_local, nnz_local, rows.ptr,
+                                    cols.ptr, vals.ptr, F64, C.byref(A)))
+    else:
+        check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
+                               None, C.byref(A)))
+    cg = C.c_void_p()
+    check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+    check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
+    total = args.warmup + args.steps
+    check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total))
+    bodies, stopped = C.c_int64(0), C.c_int(0)
+    if args.warmup:
+        check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
+    kt = not args.no_kernel_timing
+    check(L.cgx_cg_set_kernel_timing(cg, 1 if kt else 0))
+
+    # ---- timed region --------------------------------------------------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    q.wait()
+    t0 = time.perf_counter()
+    check(L.cgx_cg_run(cg, args.steps, C.byref(bodies), C.byref(stopped)))
+    q.wait()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ran = bodies.value - args.warmup
+    if ran != args.steps:
+        raise RuntimeError(f"ran {ran} iterations, expected {args.steps} (stopped={stopped.value})")
+    its = args.steps / elapsed
+    value = b_alg(n_global, nnz_global) * its / 1e9
+
+    avg = (C.c_double * 4)()
+    calls = (C.c_int64 * 4)()
+    check(L.cgx_cg_kernel_times(cg, avg, calls))
+    roof = None
+    if kt and calls[1] > 0:
+        kb = spmv_dot_bytes(n_local, nnz_local)
+        ach = kb / (avg[1] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_spmv_dot", "bytes_per_launch": kb,
+                "avg_us": round(avg[1] * 1e3, 2),
+                "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2),
+                                         "k_update_xp": round(avg[3] * 1e3, 2)}}
+        pmc = os.path.join(ROOT, "profiles", "pmc_spmv_dot.json")
+        if os.path.exists(pmc):
+            try:
+                meta = json.load(open(pmc))
+                if meta.get("grid") == n3 and meta.get("n_gpus", 1) == 1:
+                    roof["traffic"] = meta.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(n3, min(args.cpu_threads, os.cpu_count() or 1), args.cpu_budget_s)
+        line = {
+            "metric": "CG iterations/sec + achieved HBM GB/s, 256³ 7-pt Poisson fp64, "
+                      "1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "iterations_per_s": round(its, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (3-D 7-point Dirichlet Poisson CSR generated in HBM, "
+                    "b_i = i + 1, x0 = 0)",
+            "config": {"workload": f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x"
+                                   f"{nz_global}), CSR fp64/int32, fused CG iteration",
+                       "rows_global": n_global, "nnz_global": nnz_global,
+                       "bytes_per_iteration": b_alg(n_global, nnz_global),
+                       "parallelism": f"rows{world}" if world > 1 else "single"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    lib().cgx_cg_destroy(cg)
+    lib().cgx_csr_destroy(A)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,821 @@
+// cgx_abi.cpp — the C ABI of libcgx.so (include/cgx.h): contexts, memory,
+// CSR schedules, VectorOperations kernels and the fused CG driver.
+//
+// The reference drives one SYCL queue and drains it after every iteration
+// (src/CG.hpp:425, executeQueue :561-578). Here the iteration scalars live on
+// the device (CgScalars ring, cgx_internal.h), iterations are enqueued in
+// chunks (optionally replayed from a hipGraph), and the host polls the device
+// stop flag once per chunk while the next chunk is already queued.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cgx_objects.h"
+
+namespace cgx {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  set_error("%s failed: %s (%d)", what, hipGetErrorString(e), (int)e);
+  return CGX_EHIP;
+}
+
+std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz) {
+  std::vector<int> rb;
+  rb.reserve((size_t)(n / 128 + 2));
+  rb.push_back(0);
+  int64_t row = 0;
+  int mx = 0;
+  while (row < n) {
+    const int64_t start = row;
+    int len = rowptr[row + 1] - rowptr[row];
+    if (len > kTile) {  // a long row gets a workgroup of its own
+      mx = std::max(mx, len);
+      ++row;
+    } else {
+      int64_t acc = 0;
+      while (row < n && row - start < kRowsPerBlock) {
+        len = rowptr[row + 1] - rowptr[row];
+        if (acc + len > kTile) break;
+        acc += len;
+        mx = std::max(mx, len);
+        ++row;
+      }
+    }
+    rb.push_back((int)row);
+  }
+  if (max_row_nnz) *max_row_nnz = mx;
+  return rb;
+}
+
+namespace {
+
+struct DeviceGuard {
+  explicit DeviceGuard(int dev) { (void)hipSetDevice(dev); }
+};
+
+template <typename T> int enqueue_iter(cgx_cg *cg, int slot);
+
+int poll_state(cgx_cg *cg, void *h_dst, hipStream_t s) {
+  const size_t bytes = cg->dtype == CGX_F32 ? sizeof(CgScalars<float>) : sizeof(CgScalars<double>);
+  CGX_HIP(hipMemcpyAsync(h_dst, cg->st, bytes, hipMemcpyDeviceToHost, s));
+  return CGX_OK;
+}
+
+// read {active[slot], bodies, stopped, rxr[slot]} from a host copy of CgScalars
+struct StateView {
+  int active;
+  long long bodies;
+  int stopped;
+  double rxr;
+};
+StateView view_state(const cgx_cg *cg, const void *h, int slot) {
+  StateView v{};
+  if (cg->dtype == CGX_F32) {
+    const auto *s = (const CgScalars<float> *)h;
+    v = StateView{s->active[slot], s->bodies, s->stopped, (double)s->rxr[slot]};
+  } else {
+    const auto *s = (const CgScalars<double> *)h;
+    v = StateView{s->active[slot], s->bodies, s->stopped, s->rxr[slot]};
+  }
+  return v;
+}
+
+hipEvent_t next_event(cgx_cg *cg) {
+  if (cg->ev_used == cg->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    cg->ev_pool.push_back(e);
+  }
+  return cg->ev_pool[cg->ev_used++];
+}
+
+// Time one launch: records an event pair around `launch` when timing is on.
+template <class F> int timed(cgx_cg *cg, int kid, hipStream_t s, F &&launch) {
+  if (!cg->timing) {
+    CGX_HIP(launch());
+    return CGX_OK;
+  }
+  const size_t i0 = cg->ev_used;
+  hipEvent_t e0 = next_event(cg), e1 = next_event(cg);
+  CGX_REQUIRE(e0 && e1, CGX_EHIP, "hipEventCreate failed");
+  CGX_HIP(hipEventRecord(e0, s));
+  CGX_HIP(launch());
+  CGX_HIP(hipEventRecord(e1, s));
+  cg->ev_pending.emplace_back(kid, i0);
+  return CGX_OK;
+}
+
+// Accumulate pending event pairs; only the first `active_iters` iterations'
+// kernels (3 per iteration, plus an init kernel if pending) count: kernels of
+// iterations after the stop return at entry and would skew the averages.
+int harvest_events(cgx_cg *cg, int64_t active_iters) {
+  int64_t iter_seen = 0;
+  for (auto &pr : cg->ev_pending) {
+    const int kid = pr.first;
+    float ms = 0;
+    CGX_HIP(hipEventElapsedTime(&ms, cg->ev_pool[pr.second], cg->ev_pool[pr.second + 1]));
+    const bool count = kid == 0 || iter_seen < active_iters;
+    if (count) {
+      cg->t_ms[kid] += ms;
+      cg->t_calls[kid] += 1;
+    }
+    if (kid == 3) ++iter_seen;
+  }
+  cg->ev_pending.clear();
+  cg->ev_used = 0;
+  return CGX_OK;
+}
+
+template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
+  cgx_csr *A = cg->A;
+  hipStream_t s = cg->ctx->stream;
+  auto *st = (CgScalars<T> *)cg->st;
+  auto *ws = (RedWs<T> *)cg->ws;
+  T *p = (T *)cg->p, *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
+  int rc;
+  if (A->dist && A->halo.n_ghost + A->halo.send_total > 0) {
+    if ((rc = dist_halo_exchange(A, p, s))) return rc;
+  }
+  if ((rc = timed(cg, 1, s, [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s); })))
+    return rc;
+  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
+  if ((rc = timed(cg, 2, s, [&] { return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s); })))
+    return rc;
+  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
+  if ((rc = timed(cg, 3, s, [&] { return Launch<T>::update_xp(cg->n, x, p, r, st, slot, s); })))
+    return rc;
+  return CGX_OK;
+}
+
+int enqueue_iter_any(cgx_cg *cg, int slot) {
+  return cg->dtype == CGX_F32 ? enqueue_iter<float>(cg, slot) : enqueue_iter<double>(cg, slot);
+}
+
+void drop_graph(cgx_cg *cg) {
+  if (cg->graph) (void)hipGraphExecDestroy(cg->graph);
+  cg->graph = nullptr;
+}
+
+// Capture `iters` iterations (slots 0..iters-1 mod 4) as one graph.
+int build_graph(cgx_cg *cg, int iters) {
+  drop_graph(cg);
+  hipStream_t s = cg->ctx->stream;
+  CGX_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  int rc = CGX_OK;
+  for (int i = 0; i < iters && rc == CGX_OK; ++i) rc = enqueue_iter_any(cg, i & 3);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  CGX_HIP(e);
+  e = hipGraphInstantiate(&cg->graph, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  CGX_HIP(e);
+  cg->graph_x = cg->x;
+  cg->graph_iters = iters;
+  return CGX_OK;
+}
+
+bool graph_ok(const cgx_cg *cg) {
+  // RCCL calls are kept out of captured graphs; timing needs eager launches
+  return cg->use_graph && !cg->timing && !cg->A->dist && cg->poll_every % 4 == 0;
+}
+
+}  // namespace
+}  // namespace cgx
+
+using namespace cgx;
+
+// ===========================================================================
+// errors / version / devices
+// ===========================================================================
+extern "C" const char *cgx_last_error(void) { return g_err.c_str(); }
+extern "C" const char *cgx_version(void) { return "cgx 0.1.0 gfx950"; }
+
+extern "C" int cgx_device_count(int *count) {
+  CGX_REQUIRE(count, CGX_EINVAL, "count is NULL");
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *count = c;
+  return CGX_OK;
+}
+
+// ===========================================================================
+// context
+// ===========================================================================
+extern "C" int cgx_create(int device, cgx_ctx **out) {
+  CGX_REQUIRE(out, CGX_EINVAL, "out is NULL");
+  *out = nullptr;
+  int cnt = 0;
+  CGX_HIP(hipGetDeviceCount(&cnt));
+  CGX_REQUIRE(device >= 0 && device < cnt, CGX_EINVAL, "device %d out of range (%d visible)",
+              device, cnt);
+  CGX_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  CGX_HIP(hipGetDeviceProperties(&prop, device));
+  CGX_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, CGX_EUNSUPPORTED,
+              "device %d is %s; libcgx is built for gfx950 (MI355X) only", device,
+              prop.gcnArchName);
+  auto *ctx = new cgx_ctx();
+  ctx->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&ctx->ws, sizeof(RedWs<double>));
+  if (e == hipSuccess) e = hipMemset(ctx->ws, 0, sizeof(RedWs<double>));
+  if (e == hipSuccess) e = hipMalloc(&ctx->scratch, 64);
+  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_pinned, 512, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    cgx_destroy(ctx);
+    return hip_fail(e, "cgx_create");
+  }
+  *out = ctx;
+  return CGX_OK;
+}
+
+extern "C" int cgx_destroy(cgx_ctx *ctx) {
+  if (!ctx) return CGX_OK;
+  DeviceGuard g(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  dist_comm_destroy(ctx);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return CGX_OK;
+}
+
+extern "C" int cgx_sync(cgx_ctx *ctx) {
+  CGX_REQUIRE(ctx, CGX_EINVAL, "ctx is NULL");
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_get_stream(cgx_ctx *ctx, void **s) {
+  CGX_REQUIRE(ctx && s, CGX_EINVAL, "NULL argument");
+  *s = (void *)ctx->stream;
+  return CGX_OK;
+}
+
+extern "C" int cgx_get_device(cgx_ctx *ctx, int *d) {
+  CGX_REQUIRE(ctx && d, CGX_EINVAL, "NULL argument");
+  *d = ctx->device;
+  return CGX_OK;
+}
+
+// ===========================================================================
+// memory
+// ===========================================================================
+extern "C" int cgx_alloc(cgx_ctx *ctx, size_t bytes, void **d_out) {
+  CGX_REQUIRE(ctx && d_out, CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  *d_out = nullptr;
+  hipError_t e = hipMalloc(d_out, bytes ? bytes : 1);
+  if (e == hipErrorOutOfMemory) {
+    set_error("hipMalloc(%zu) out of device memory", bytes);
+    return CGX_ENOMEM;
+  }
+  CGX_HIP(e);
+  return CGX_OK;
+}
+
+extern "C" int cgx_free(cgx_ctx *ctx, void *d) {
+  CGX_REQUIRE(ctx, CGX_EINVAL, "ctx is NULL");
+  if (!d) return CGX_OK;
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  CGX_HIP(hipFree(d));
+  return CGX_OK;
+}
+
+extern "C" int cgx_h2d(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_h2d_async(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_d2h(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_d2d(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
+  CGX_REQUIRE(ctx && (n == 0 || d), CGX_EINVAL, "NULL argument");
+  if (n == 0) return CGX_OK;
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32) CGX_HIP(Launch<float>::fill((float *)d, (float)v, (int64_t)n, ctx->stream));
+  else CGX_HIP(Launch<double>::fill((double *)d, v, (int64_t)n, ctx->stream));
+  return CGX_OK;
+}
+
+// ===========================================================================
+// CSR
+// ===========================================================================
+extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d_rowptr,
+                              const int *d_col, const void *d_val, int dtype,
+                              const int *h_rowptr, cgx_csr **out) {
+  CGX_REQUIRE(ctx && out && d_rowptr, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(n >= 1 && n < (int64_t(1) << 31) - 1, CGX_EINVAL, "n=%lld out of range",
+              (long long)n);
+  CGX_REQUIRE(nnz >= 0 && nnz < (int64_t(1) << 31), CGX_EINVAL, "nnz=%lld out of range",
+              (long long)nnz);
+  CGX_REQUIRE(nnz == 0 || (d_col && d_val), CGX_EINVAL, "NULL column/value arrays");
+  CGX_REQUIRE(dtype == CGX_F64 || dtype == CGX_F32, CGX_EINVAL, "bad dtype %d", dtype);
+  DeviceGuard g(ctx->device);
+  *out = nullptr;
+  std::vector<int> hrp;
+  if (!h_rowptr) {
+    hrp.resize((size_t)n + 1);
+    CGX_HIP(hipMemcpyAsync(hrp.data(), d_rowptr, ((size_t)n + 1) * sizeof(int),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    CGX_HIP(hipStreamSynchronize(ctx->stream));
+    h_rowptr = hrp.data();
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    if (h_rowptr[i + 1] < h_rowptr[i]) {
+      set_error("rowptr is not monotone at row %lld", (long long)i);
+      return CGX_EINVAL;
+    }
+  }
+  CGX_REQUIRE(h_rowptr[0] >= 0 && h_rowptr[n] <= nnz, CGX_EINVAL,
+              "rowptr range [%d, %d] outside [0, nnz=%lld]", h_rowptr[0], h_rowptr[n],
+              (long long)nnz);
+  int mx = 0;
+  std::vector<int> rb = build_row_blocks(h_rowptr, n, &mx);
+  auto *A = new cgx_csr();
+  A->ctx = ctx;
+  A->dtype = dtype;
+  A->max_row_nnz = mx;
+  A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, (int)rb.size() - 1};
+  hipError_t e = hipMalloc(&A->d_rb, rb.size() * sizeof(int));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    cgx_csr_destroy(A);
+    return hip_fail(e, "cgx_csr_create");
+  }
+  A->dev.rb = A->d_rb;
+  A->n_global = n;
+  *out = A;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_destroy(cgx_csr *A) {
+  if (!A) return CGX_OK;
+  DeviceGuard g(A->ctx->device);
+  (void)hipStreamSynchronize(A->ctx->stream);
+  if (A->d_rb) (void)hipFree(A->d_rb);
+  if (A->d_ext) (void)hipFree(A->d_ext);
+  dist_destroy_halo(A);
+  delete A;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, int *mx) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  if (n) *n = A->dev.n;
+  if (nnz) *nnz = A->dev.nnz;
+  if (rbs) *rbs = A->dev.nrb;
+  if (mx) *mx = A->max_row_nnz;
+  return CGX_OK;
+}
+
+// x with ghost values for a distributed matrix: copy into A->d_ext + exchange
+static int dist_extend(cgx_csr *A, const void *d_x, const void **x_ext) {
+  *x_ext = d_x;
+  if (!A->dist) return CGX_OK;
+  const size_t es = dtype_size(A->dtype);
+  if (!A->d_ext) CGX_HIP(hipMalloc(&A->d_ext, (size_t)(A->dev.n + A->halo.n_ghost + 1) * es));
+  CGX_HIP(hipMemcpyAsync(A->d_ext, d_x, (size_t)A->dev.n * es, hipMemcpyDeviceToDevice,
+                         A->ctx->stream));
+  int rc = dist_halo_exchange(A, A->d_ext, A->ctx->stream);
+  if (rc) return rc;
+  *x_ext = A->d_ext;
+  return CGX_OK;
+}
+
+// ===========================================================================
+// VectorOperations
+// ===========================================================================
+extern "C" int cgx_spmv(cgx_ctx *ctx, cgx_csr *A, const void *x, void *y, int64_t count) {
+  CGX_REQUIRE(ctx && A && x && y, CGX_EINVAL, "NULL argument");
+  // VectorOperations.hpp:444: assert(vector_size != 0 && A.N() == vector_size)
+  CGX_REQUIRE(count == A->dev.n, CGX_EINVAL, "spmv count %lld != A.N() %lld",
+              (long long)count, (long long)A->dev.n);
+  DeviceGuard g(ctx->device);
+  const void *xe = x;
+  int rc = dist_extend(A, x, &xe);
+  if (rc) return rc;
+  if (A->dtype == CGX_F32)
+    CGX_HIP(Launch<float>::spmv(A->dev, (const float *)xe, (float *)y, ctx->stream));
+  else
+    CGX_HIP(Launch<double>::spmv(A->dev, (const double *)xe, (double *)y, ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_dot_acc(cgx_ctx *ctx, int dtype, int64_t n, const void *x, const void *y,
+                           void *res) {
+  CGX_REQUIRE(ctx && x && y && res && n >= 0, CGX_EINVAL, "bad argument");
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32)
+    CGX_HIP(Launch<float>::dot_acc(n, (const float *)x, (const float *)y, (float *)res,
+                                   (RedWs<float> *)ctx->ws, ctx->stream));
+  else
+    CGX_HIP(Launch<double>::dot_acc(n, (const double *)x, (const double *)y, (double *)res,
+                                    (RedWs<double> *)ctx->ws, ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_norm_acc(cgx_ctx *ctx, int dtype, int64_t n, const void *x, void *res) {
+  return cgx_dot_acc(ctx, dtype, n, x, x, res);
+}
+
+static int axpby_any(cgx_ctx *ctx, int mode, int dtype, int64_t n, const void *x,
+                     const void *y, const void *a, const void *b, void *res) {
+  CGX_REQUIRE(ctx && x && y && b && res && n >= 0, CGX_EINVAL, "bad argument");
+  CGX_REQUIRE(mode != AX_SAXPBY || a, CGX_EINVAL, "saxpby needs a");
+  if (n == 0) return CGX_OK;
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32)
+    CGX_HIP(Launch<float>::axpby(mode, n, (const float *)x, (const float *)y,
+                                 (const float *)a, (const float *)b, (float *)res,
+                                 ctx->stream));
+  else
+    CGX_HIP(Launch<double>::axpby(mode, n, (const double *)x, (const double *)y,
+                                  (const double *)a, (const double *)b, (double *)res,
+                                  ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_sapbx(cgx_ctx *ctx, int dtype, int64_t n, const void *x, const void *y,
+                         const void *b, void *res) {
+  return axpby_any(ctx, AX_SAPBX, dtype, n, x, y, nullptr, b, res);
+}
+extern "C" int cgx_sambx(cgx_ctx *ctx, int dtype, int64_t n, const void *x, const void *y,
+                         const void *b, void *res) {
+  return axpby_any(ctx, AX_SAMBX, dtype, n, x, y, nullptr, b, res);
+}
+extern "C" int cgx_saxpby(cgx_ctx *ctx, int dtype, int64_t n, const void *x, const void *y,
+                          const void *a, const void *b, void *res) {
+  return axpby_any(ctx, AX_SAXPBY, dtype, n, x, y, a, b, res);
+}
+
+extern "C" int cgx_scalar_div(cgx_ctx *ctx, int dtype, const void *num, const void *den,
+                              void *out) {
+  CGX_REQUIRE(ctx && num && den && out, CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32)
+    CGX_HIP(Launch<float>::scalar_div((const float *)num, (const float *)den, (float *)out,
+                                      ctx->stream));
+  else
+    CGX_HIP(Launch<double>::scalar_div((const double *)num, (const double *)den,
+                                       (double *)out, ctx->stream));
+  return CGX_OK;
+}
+
+// ===========================================================================
+// fused CG
+// ===========================================================================
+extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
+  CGX_REQUIRE(ctx && A && out, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(A->ctx == ctx, CGX_EINVAL, "matrix belongs to another context");
+  DeviceGuard g(ctx->device);
+  *out = nullptr;
+  auto *cg = new cgx_cg();
+  cg->ctx = ctx;
+  cg->A = A;
+  cg->dtype = A->dtype;
+  cg->n = A->dev.n;
+  const size_t es = dtype_size(cg->dtype);
+  const size_t next = (size_t)(cg->n + A->halo.n_ghost);
+  const size_t stb = cg->dtype == CGX_F32 ? sizeof(CgScalars<float>) : sizeof(CgScalars<double>);
+  const size_t wsb = cg->dtype == CGX_F32 ? sizeof(RedWs<float>) : sizeof(RedWs<double>);
+  hipError_t e = hipMalloc(&cg->r, (size_t)cg->n * es);
+  if (e == hipSuccess) e = hipMalloc(&cg->p, next * es);
+  if (e == hipSuccess) e = hipMalloc(&cg->Ap, next * es);
+  if (e == hipSuccess) e = hipMalloc(&cg->st, stb);
+  if (e == hipSuccess) e = hipMalloc(&cg->ws, wsb);
+  if (e == hipSuccess) e = hipMemsetAsync(cg->st, 0, stb, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(cg->ws, 0, wsb, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(cg->p, 0, next * es, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    cgx_cg_destroy(cg);
+    if (e == hipErrorOutOfMemory) {
+      set_error("cgx_cg_create: out of device memory (n=%lld)", (long long)cg->n);
+      return CGX_ENOMEM;
+    }
+    return hip_fail(e, "cgx_cg_create");
+  }
+  *out = cg;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_destroy(cgx_cg *cg) {
+  if (!cg) return CGX_OK;
+  DeviceGuard g(cg->ctx->device);
+  (void)hipStreamSynchronize(cg->ctx->stream);
+  drop_graph(cg);
+  for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
+  for (void *p : {cg->r, cg->p, cg->Ap, cg->st, cg->ws})
+    if (p) (void)hipFree(p);
+  delete cg;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  if (poll_every > 0) {
+    if (poll_every != cg->poll_every) drop_graph(cg);
+    cg->poll_every = poll_every;
+  }
+  if (use_graph >= 0) cg->use_graph = use_graph != 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
+                            int64_t max_bodies) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  // CG.hpp:266-272
+  CGX_REQUIRE(b, CGX_ESTATE, "No right hand side to solve for");
+  CGX_REQUIRE(x, CGX_EINVAL, "x is NULL");
+  DeviceGuard g(cg->ctx->device);
+  cgx_csr *A = cg->A;
+  hipStream_t s = cg->ctx->stream;
+  const int64_t n_ref = (A->dist ? A->n_global : A->dev.n);
+  long long cap = (long long)n_ref + 1;  // counter++ < N  (CG.hpp:436)
+  if (max_bodies >= 0) cap = std::min<long long>(cap, std::max<long long>(max_bodies, 1));
+  cg->b = b;
+  cg->x = x;
+  const void *xe = x;
+  int rc;
+  if (A->dist) {
+    // initial guess with ghost values, staged in the Ap buffer (free at init)
+    const size_t es = dtype_size(cg->dtype);
+    CGX_HIP(hipMemcpyAsync(cg->Ap, x, (size_t)cg->n * es, hipMemcpyDeviceToDevice, s));
+    if ((rc = dist_halo_exchange(A, cg->Ap, s))) return rc;
+    xe = cg->Ap;
+  }
+  rc = timed(cg, 0, s, [&] {
+    if (cg->dtype == CGX_F32)
+      return Launch<float>::cg_init(A->dev, (const float *)xe, (const float *)b, (float *)cg->r,
+                                    (float *)cg->p, (CgScalars<float> *)cg->st,
+                                    (RedWs<float> *)cg->ws, (float)tol, cap, s);
+    return Launch<double>::cg_init(A->dev, (const double *)xe, (const double *)b,
+                                   (double *)cg->r, (double *)cg->p,
+                                   (CgScalars<double> *)cg->st, (RedWs<double> *)cg->ws, tol,
+                                   cap, s);
+  });
+  if (rc) return rc;
+  if (A->dist) {
+    const size_t off = cg->dtype == CGX_F32 ? offsetof(CgScalars<float>, rxr)
+                                            : offsetof(CgScalars<double>, rxr);
+    if ((rc = dist_allreduce_scalar(cg->ctx, (char *)cg->st + off, cg->dtype, 1, s))) return rc;
+  }
+  cg->slot = 0;
+  cg->begun = true;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int *stopped) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  CGX_REQUIRE(cg->begun, CGX_ESTATE, "cgx_cg_run before cgx_cg_begin");
+  DeviceGuard g(cg->ctx->device);
+  hipStream_t s = cg->ctx->stream;
+  const bool use_graph = graph_ok(cg);
+  if (use_graph && cg->graph && (cg->graph_x != cg->x || cg->graph_iters != cg->poll_every))
+    drop_graph(cg);
+  // Two host staging buffers: chunk c's state is read while chunk c+1 runs.
+  auto *hbuf = (char *)cg->ctx->h_pinned;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  CGX_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  CGX_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  struct Pending { int buf; int slot_after; int64_t iters; };
+  std::vector<Pending> q;
+  int64_t remaining = bodies;
+  int chunk_id = 0, rc = CGX_OK;
+  bool done = false;
+  long long last_bodies = -1;
+  int last_stopped = 0;
+  long long bodies_before = -1;
+  auto wait_one = [&]() -> int {
+    Pending pd = q.front();
+    q.erase(q.begin());
+    CGX_HIP(hipEventSynchronize(ev[pd.buf]));
+    StateView v = view_state(cg, hbuf + 256 * pd.buf, pd.slot_after);
+    if (cg->timing) {
+      const long long before = bodies_before < 0 ? 0 : bodies_before;
+      (void)before;
+    }
+    last_bodies = v.bodies;
+    last_stopped = v.stopped;
+    if (!v.active) done = true;
+    return CGX_OK;
+  };
+  // bodies executed before this call (for the timing harvest)
+  if (cg->timing) {
+    CGX_HIP(hipStreamSynchronize(s));
+    if ((rc = poll_state(cg, hbuf, s))) return rc;
+    CGX_HIP(hipStreamSynchronize(s));
+    bodies_before = view_state(cg, hbuf, cg->slot).bodies;
+    // an init kernel may still be pending in the event list
+  }
+  while (!done && (remaining > 0 || !q.empty())) {
+    if (remaining > 0 && q.size() < 2) {
+      int64_t chunk;
+      if (use_graph && cg->slot == 0 && remaining >= cg->poll_every) {
+        if (!cg->graph && (rc = build_graph(cg, cg->poll_every))) break;
+        CGX_HIP(hipGraphLaunch(cg->graph, s));
+        chunk = cg->poll_every;
+      } else {
+        chunk = std::min<int64_t>(remaining, cg->poll_every);
+        for (int64_t i = 0; i < chunk && rc == CGX_OK; ++i) rc = enqueue_iter_any(cg, (cg->slot + (int)i) & 3);
+        if (rc) break;
+      }
+      cg->slot = (int)((cg->slot + chunk) & 3);
+      remaining -= chunk;
+      const int buf = chunk_id++ & 1;
+      if ((rc = poll_state(cg, hbuf + 256 * buf, s))) break;
+      CGX_HIP(hipEventRecord(ev[buf], s));
+      q.push_back(Pending{buf, cg->slot, chunk});
+      continue;
+    }
+    if ((rc = wait_one())) break;
+  }
+  // drain whatever is still queued
+  while (rc == CGX_OK && !q.empty()) rc = wait_one();
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  if (rc) return rc;
+  if (cg->timing) {
+    CGX_HIP(hipStreamSynchronize(s));
+    const int64_t active_iters = last_bodies - (bodies_before < 0 ? 0 : bodies_before);
+    if ((rc = harvest_events(cg, active_iters))) return rc;
+  }
+  if (bodies_total) *bodies_total = last_bodies;
+  if (stopped) *stopped = last_stopped;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_solve(cgx_cg *cg, const void *b, void *x, double tol, int64_t max_bodies,
+                            int64_t *bodies_out, double *rxr_out) {
+  int rc = cgx_cg_begin(cg, b, x, tol, max_bodies);
+  if (rc) return rc;
+  const int64_t n_ref = cg->A->dist ? cg->A->n_global : cg->n;
+  int64_t cap = n_ref + 1;
+  if (max_bodies >= 0) cap = std::min<int64_t>(cap, std::max<int64_t>(max_bodies, 1));
+  int64_t total = 0;
+  int stopped = 0;
+  if ((rc = cgx_cg_run(cg, cap, &total, &stopped))) return rc;
+  DeviceGuard g(cg->ctx->device);
+  if (rxr_out) {
+    // the rxr after the last body sits in the slot of the first skipped body
+    auto *h = (char *)cg->ctx->h_pinned;
+    if ((rc = poll_state(cg, h, cg->ctx->stream))) return rc;
+    CGX_HIP(hipStreamSynchronize(cg->ctx->stream));
+    *rxr_out = view_state(cg, h, (int)(total & 3)).rxr;
+  }
+  if (bodies_out) *bodies_out = total;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  cg->timing = enable != 0;
+  for (int i = 0; i < 4; ++i) {
+    cg->t_ms[i] = 0;
+    cg->t_calls[i] = 0;
+  }
+  cg->ev_pending.clear();
+  cg->ev_used = 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  DeviceGuard g(cg->ctx->device);
+  if (!cg->ev_pending.empty()) {  // an init kernel timed outside cgx_cg_run
+    CGX_HIP(hipStreamSynchronize(cg->ctx->stream));
+    int rc = harvest_events(cg, 0);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < 4; ++i) {
+    if (avg_ms) avg_ms[i] = cg->t_calls[i] ? cg->t_ms[i] / (double)cg->t_calls[i] : 0.0;
+    if (calls) calls[i] = cg->t_calls[i];
+  }
+  return CGX_OK;
+}
+
+// ===========================================================================
+// accuracy (CG.hpp:463-515)
+// ===========================================================================
+extern "C" int cgx_accuracy(cgx_ctx *ctx, cgx_csr *A, const void *b, const void *x,
+                            double *out) {
+  CGX_REQUIRE(ctx && A && b && x && out, CGX_EINVAL, "NULL argument");
+  DeviceGuard g(ctx->device);
+  const void *xe = x;
+  int rc = dist_extend(A, x, &xe);
+  if (rc) return rc;
+  double h[2];
+  if (A->dtype == CGX_F32) {
+    CGX_HIP(Launch<float>::accuracy(A->dev, (const float *)b, (const float *)xe,
+                                    (float *)ctx->scratch, (RedWs<float> *)ctx->ws,
+                                    ctx->stream));
+    if (A->dist && (rc = dist_allreduce_scalar(ctx, ctx->scratch, CGX_F32, 2, ctx->stream)))
+      return rc;
+    float hf[2];
+    CGX_HIP(hipMemcpyAsync(hf, ctx->scratch, sizeof(hf), hipMemcpyDeviceToHost, ctx->stream));
+    CGX_HIP(hipStreamSynchronize(ctx->stream));
+    h[0] = hf[0];
+    h[1] = hf[1];
+    *out = (double)std::fabs(hf[0] / hf[1]);
+    return CGX_OK;
+  }
+  CGX_HIP(Launch<double>::accuracy(A->dev, (const double *)b, (const double *)xe,
+                                   (double *)ctx->scratch, (RedWs<double> *)ctx->ws,
+                                   ctx->stream));
+  if (A->dist && (rc = dist_allreduce_scalar(ctx, ctx->scratch, CGX_F64, 2, ctx->stream)))
+    return rc;
+  CGX_HIP(hipMemcpyAsync(h, ctx->scratch, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  *out = std::fabs(h[0] / h[1]);
+  return CGX_OK;
+}
+
+// ===========================================================================
+// synthetic inputs
+// ===========================================================================
+extern "C" int64_t cgx_poisson_nnz(int dim, int nx, int ny, int nz, int64_t row_begin,
+                                   int64_t row_end) {
+  if (dim != 2 && dim != 3) return -1;
+  return poisson_row_offset(dim, nx, ny, dim == 3 ? nz : 1, row_end) -
+         poisson_row_offset(dim, nx, ny, dim == 3 ? nz : 1, row_begin);
+}
+
+extern "C" int cgx_poisson_fill(cgx_ctx *ctx, int dtype, int dim, int nx, int ny, int nz,
+                                int64_t row_begin, int64_t row_end, int *d_rowptr, int *d_col,
+                                void *d_val) {
+  CGX_REQUIRE(ctx && d_rowptr && d_col && d_val, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(dim == 2 || dim == 3, CGX_EINVAL, "dim must be 2 or 3");
+  CGX_REQUIRE(nx > 0 && ny > 0 && (dim == 2 || nz > 0), CGX_EINVAL, "bad grid");
+  const int zz = dim == 3 ? nz : 1;
+  const int64_t n = (int64_t)nx * ny * zz;
+  CGX_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n, CGX_EINVAL,
+              "bad row range");
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32)
+    CGX_HIP(Launch<float>::poisson(dim, nx, ny, zz, row_begin, row_end, d_rowptr, d_col,
+                                   (float *)d_val, ctx->stream));
+  else
+    CGX_HIP(Launch<double>::poisson(dim, nx, ny, zz, row_begin, row_end, d_rowptr, d_col,
+                                    (double *)d_val, ctx->stream));
+  return CGX_OK;
+}
+
+extern "C" int cgx_iota(cgx_ctx *ctx, int dtype, void *d_b, int64_t n, double offset) {
+  CGX_REQUIRE(ctx && d_b && n >= 0, CGX_EINVAL, "bad argument");
+  if (n == 0) return CGX_OK;
+  DeviceGuard g(ctx->device);
+  if (dtype == CGX_F32) CGX_HIP(Launch<float>::iota((float *)d_b, n, offset, ctx->stream));
+  else CGX_HIP(Launch<double>::iota((double *)d_b, n, offset, ctx->stream));
+  return CGX_OK;
+}

@@ -1,0 +1,365 @@
+// cgx_dist.cpp — row-partitioned CG across the GPUs of one node (SURVEY.md
+// §8(e)): one process per GPU, one RCCL communicator, contiguous row blocks.
+//
+// The reference is single-device; this file adds the
+// partition. Per iteration:
+//   * halo exchange of p: every rank packs the p entries its neighbours need
+//     (k_gather) and ncclSend/ncclRecv's them inside one group; received
+//     values land in p's ghost area [n_local, n_local + n_ghost), grouped by
+//     owner, so the SpMV reads local and ghost entries from one array;
+//   * ncclAllReduce of p.Ap and r.r (one scalar each, in place on the device
+//     scalar ring; every rank then derives identical alpha / beta / stop).
+// Setup (cgx_csr_create_dist) builds the plan from the local rows' global
+// column indices with the host-only helpers cgx_plan_ghosts/cgx_plan_remap,
+// which the CPU test-suite drives directly over a gloo world.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "cgx_objects.h"
+
+namespace cgx {
+
+static int nccl_fail(ncclResult_t r, const char *what) {
+  set_error("%s failed: %s", what, ncclGetErrorString(r));
+  return CGX_ENCCL;
+}
+
+#define CGX_NCCL(expr)                                          \
+  do {                                                          \
+    ncclResult_t r_ = (expr);                                   \
+    if (r_ != ncclSuccess) return ::cgx::nccl_fail(r_, #expr);  \
+  } while (0)
+
+static ncclDataType_t nccl_type(int dtype) { return dtype == CGX_F32 ? ncclFloat : ncclDouble; }
+
+int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
+  if (!A->dist) return CGX_OK;
+  cgx_ctx *ctx = A->ctx;
+  Halo &h = A->halo;
+  if (ctx->world == 1 || (h.n_ghost == 0 && h.send_total == 0)) return CGX_OK;
+  const size_t es = dtype_size(A->dtype);
+  if (h.send_total > 0) {
+    if (A->dtype == CGX_F32)
+      CGX_HIP(Launch<float>::gather((const float *)vec_ext, h.d_send_idx, h.send_total,
+                                    (float *)h.d_send_buf, s));
+    else
+      CGX_HIP(Launch<double>::gather((const double *)vec_ext, h.d_send_idx, h.send_total,
+                                     (double *)h.d_send_buf, s));
+  }
+  const ncclDataType_t t = nccl_type(A->dtype);
+  CGX_NCCL(ncclGroupStart());
+  for (size_t i = 0; i < h.nbr.size(); ++i) {
+    if (h.send_cnt[i] > 0)
+      CGX_NCCL(ncclSend((char *)h.d_send_buf + (size_t)h.send_off[i] * es,
+                        (size_t)h.send_cnt[i], t, h.nbr[i], ctx->comm, s));
+    if (h.recv_cnt[i] > 0)
+      CGX_NCCL(ncclRecv((char *)vec_ext + (size_t)(A->dev.n + h.recv_off[i]) * es,
+                        (size_t)h.recv_cnt[i], t, h.nbr[i], ctx->comm, s));
+  }
+  CGX_NCCL(ncclGroupEnd());
+  return CGX_OK;
+}
+
+int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s) {
+  if (!ctx->comm || ctx->world == 1) return CGX_OK;
+  CGX_NCCL(ncclAllReduce(d_val, d_val, (size_t)count, nccl_type(dtype), ncclSum, ctx->comm, s));
+  return CGX_OK;
+}
+
+int dist_destroy_halo(cgx_csr *A) {
+  if (A->halo.d_send_idx) (void)hipFree(A->halo.d_send_idx);
+  if (A->halo.d_send_buf) (void)hipFree(A->halo.d_send_buf);
+  A->halo.d_send_idx = nullptr;
+  A->halo.d_send_buf = nullptr;
+  return CGX_OK;
+}
+
+int dist_comm_destroy(cgx_ctx *ctx) {
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  ctx->comm = nullptr;
+  return CGX_OK;
+}
+
+}  // namespace cgx
+
+using namespace cgx;
+
+// ===========================================================================
+// host-only plan helpers (no device access; usable without a GPU)
+// ===========================================================================
+
+// Ghost columns of a local row block: the sorted distinct global columns
+// outside [row_begin, row_begin + n_local), and how many of them each rank
+// owns (begins/counts: every rank's row range, indexed by rank).
+extern "C" int cgx_plan_ghosts(int64_t n_local, int64_t row_begin, int64_t nnz, const int *col,
+                               int world, const int64_t *begins, const int64_t *counts,
+                               int64_t *n_ghost, int64_t **ghosts, int64_t *recv_cnt) {
+  CGX_REQUIRE(col || nnz == 0, CGX_EINVAL, "col is NULL");
+  CGX_REQUIRE(n_ghost && ghosts && recv_cnt && begins && counts && world >= 1, CGX_EINVAL,
+              "NULL argument");
+  const int64_t lo = row_begin, hi = row_begin + n_local;
+  std::vector<int64_t> g;
+  for (int64_t k = 0; k < nnz; ++k) {
+    const int64_t c = col[k];
+    if (c < lo || c >= hi) g.push_back(c);
+  }
+  std::sort(g.begin(), g.end());
+  g.erase(std::unique(g.begin(), g.end()), g.end());
+  std::fill(recv_cnt, recv_cnt + world, 0);
+  for (int64_t c : g) {
+    int owner = -1;
+    for (int r = 0; r < world; ++r)
+      if (c >= begins[r] && c < begins[r] + counts[r]) { owner = r; break; }
+    CGX_REQUIRE(owner >= 0, CGX_EINVAL, "column %lld is owned by no rank", (long long)c);
+    recv_cnt[owner] += 1;
+  }
+  // ghosts sorted by global index are grouped by owner only when the row
+  // ranges are ordered by rank; cgx_csr_create_dist requires that.
+  for (int r = 1; r < world; ++r)
+    CGX_REQUIRE(begins[r] >= begins[r - 1] + counts[r - 1], CGX_EINVAL,
+                "row ranges must be contiguous and ordered by rank");
+  *n_ghost = (int64_t)g.size();
+  *ghosts = (int64_t *)std::malloc(std::max<size_t>(g.size(), 1) * sizeof(int64_t));
+  std::copy(g.begin(), g.end(), *ghosts);
+  return CGX_OK;
+}
+
+// Rewrite global columns to local numbering: own rows -> c - row_begin,
+// ghosts -> n_local + position in the sorted ghost list.
+extern "C" int cgx_plan_remap(int64_t n_local, int64_t row_begin, int64_t nnz, int *col,
+                              int64_t n_ghost, const int64_t *ghosts) {
+  CGX_REQUIRE(col || nnz == 0, CGX_EINVAL, "col is NULL");
+  const int64_t lo = row_begin, hi = row_begin + n_local;
+  for (int64_t k = 0; k < nnz; ++k) {
+    const int64_t c = col[k];
+    if (c >= lo && c < hi) {
+      col[k] = (int)(c - lo);
+    } else {
+      const int64_t *it = std::lower_bound(ghosts, ghosts + n_ghost, c);
+      CGX_REQUIRE(it != ghosts + n_ghost && *it == c, CGX_EINVAL,
+                  "column %lld missing from ghost list", (long long)c);
+      col[k] = (int)(n_local + (it - ghosts));
+    }
+  }
+  return CGX_OK;
+}
+
+extern "C" void cgx_free_host(void *p) { std::free(p); }
+
+extern "C" int cgx_row_blocks(const int *rowptr, int64_t n, int64_t *nrb, int **rb,
+                              int *max_row_nnz) {
+  CGX_REQUIRE(rowptr && nrb && rb, CGX_EINVAL, "NULL argument");
+  std::vector<int> v = build_row_blocks(rowptr, n, max_row_nnz);
+  *nrb = (int64_t)v.size() - 1;
+  *rb = (int *)std::malloc(v.size() * sizeof(int));
+  std::copy(v.begin(), v.end(), *rb);
+  return CGX_OK;
+}
+
+// ===========================================================================
+// RCCL communicator
+// ===========================================================================
+extern "C" int cgx_nccl_unique_id(char *id_out, size_t len) {
+  CGX_REQUIRE(id_out && len >= sizeof(ncclUniqueId), CGX_EINVAL, "buffer too small (%zu < %zu)",
+              len, sizeof(ncclUniqueId));
+  ncclUniqueId id;
+  CGX_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return CGX_OK;
+}
+
+extern "C" int cgx_dist_init(cgx_ctx *ctx, int rank, int world, const char *id, size_t len) {
+  CGX_REQUIRE(ctx && id && len >= sizeof(ncclUniqueId), CGX_EINVAL, "bad argument");
+  CGX_REQUIRE(world >= 1 && rank >= 0 && rank < world, CGX_EINVAL, "bad rank/world");
+  CGX_REQUIRE(!ctx->comm, CGX_ESTATE, "communicator already initialised");
+  CGX_HIP(hipSetDevice(ctx->device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t comm = nullptr;
+  CGX_NCCL(ncclCommInitRank(&comm, world, uid, rank));
+  ctx->comm = comm;
+  ctx->rank = rank;
+  ctx->world = world;
+  return CGX_OK;
+}
+
+extern "C" int cgx_dist_rank(cgx_ctx *ctx, int *rank, int *world) {
+  CGX_REQUIRE(ctx && rank && world, CGX_EINVAL, "NULL argument");
+  *rank = ctx->rank;
+  *world = ctx->world;
+  return CGX_OK;
+}
+
+extern "C" int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value) {
+  CGX_REQUIRE(ctx && value, CGX_EINVAL, "NULL argument");
+  if (!ctx->comm || ctx->world == 1) return CGX_OK;
+  CGX_HIP(hipSetDevice(ctx->device));
+  CGX_HIP(hipMemcpyAsync(ctx->scratch, value, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  CGX_NCCL(ncclAllReduce(ctx->scratch, ctx->scratch, 1, ncclDouble, ncclSum, ctx->comm,
+                         ctx->stream));
+  CGX_HIP(hipMemcpyAsync(value, ctx->scratch, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  return CGX_OK;
+}
+
+// ===========================================================================
+// distributed CSR
+// ===========================================================================
+extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_begin,
+                                   int64_t n_local, int64_t nnz_local, const int *d_rowptr,
+                                   int *d_col, const void *d_val, int dtype, cgx_csr **out) {
+  CGX_REQUIRE(ctx && out && d_rowptr && d_col && d_val, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(ctx->comm || ctx->world == 1, CGX_ESTATE, "cgx_dist_init first");
+  CGX_REQUIRE(n_local >= 1 && row_begin >= 0 && row_begin + n_local <= n_global, CGX_EINVAL,
+              "bad local row range");
+  CGX_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int world = ctx->world, me = ctx->rank;
+  // 1. every rank's row range
+  std::vector<int64_t> part(2 * (size_t)world, 0);
+  {
+    int64_t mine[2] = {row_begin, n_local};
+    void *d = nullptr;
+    CGX_HIP(hipMalloc(&d, part.size() * sizeof(int64_t)));
+    CGX_HIP(hipMemcpyAsync((int64_t *)d + 2 * me, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+    if (world > 1)
+      CGX_NCCL(ncclAllGather((int64_t *)d + 2 * me, d, 2, ncclInt64, ctx->comm, s));
+    CGX_HIP(hipMemcpyAsync(part.data(), d, part.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(d);
+  }
+  std::vector<int64_t> begins(world), counts(world);
+  for (int r = 0; r < world; ++r) {
+    begins[r] = part[2 * r];
+    counts[r] = part[2 * r + 1];
+  }
+  // 2. local structure to the host
+  std::vector<int> hrp((size_t)n_local + 1), hcol((size_t)nnz_local);
+  CGX_HIP(hipMemcpyAsync(hrp.data(), d_rowptr, hrp.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipMemcpyAsync(hcol.data(), d_col, hcol.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  int64_t n_ghost = 0;
+  int64_t *ghosts = nullptr;
+  std::vector<int64_t> recv_cnt(world, 0);
+  int rc = cgx_plan_ghosts(n_local, row_begin, nnz_local, hcol.data(), world, begins.data(),
+                           counts.data(), &n_ghost, &ghosts, recv_cnt.data());
+  if (rc) return rc;
+  // 3. all-to-all of counts via an all-gather of the world x world matrix
+  std::vector<int64_t> cmat((size_t)world * world, 0);
+  {
+    void *d = nullptr;
+    CGX_HIP(hipMalloc(&d, cmat.size() * sizeof(int64_t)));
+    CGX_HIP(hipMemcpyAsync((int64_t *)d + (size_t)world * me, recv_cnt.data(),
+                           world * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (world > 1)
+      CGX_NCCL(ncclAllGather((int64_t *)d + (size_t)world * me, d, (size_t)world, ncclInt64,
+                             ctx->comm, s));
+    CGX_HIP(hipMemcpyAsync(cmat.data(), d, cmat.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(d);
+  }
+  // 4. request lists: I send the global ids I need to each owner
+  auto *A = new cgx_csr();
+  A->ctx = ctx;
+  A->dtype = dtype;
+  A->dist = true;
+  A->n_global = n_global;
+  A->row_begin = row_begin;
+  Halo &h = A->halo;
+  h.n_ghost = n_ghost;
+  int64_t roff = 0, soff = 0;
+  for (int r = 0; r < world; ++r) {
+    const int64_t rc_ = recv_cnt[r], sc_ = cmat[(size_t)r * world + me];
+    if (r == me || (rc_ == 0 && sc_ == 0)) continue;
+    h.nbr.push_back(r);
+    h.recv_cnt.push_back(rc_);
+    h.recv_off.push_back(roff);
+    h.send_cnt.push_back(sc_);
+    h.send_off.push_back(soff);
+    roff += rc_;
+    soff += sc_;
+  }
+  h.send_total = soff;
+  {
+    std::vector<int> greq((size_t)std::max<int64_t>(n_ghost, 1));
+    for (int64_t i = 0; i < n_ghost; ++i) greq[i] = (int)ghosts[i];
+    int *d_req = nullptr, *d_inc = nullptr;
+    hipError_t e = hipMalloc(&d_req, greq.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&d_inc, (size_t)std::max<int64_t>(soff, 1) * sizeof(int));
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_req, greq.data(), greq.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      cgx_free_host(ghosts);
+      cgx_csr_destroy(A);
+      return hip_fail(e, "cgx_csr_create_dist(requests)");
+    }
+    if (!h.nbr.empty()) {
+      CGX_NCCL(ncclGroupStart());
+      for (size_t i = 0; i < h.nbr.size(); ++i) {
+        if (h.recv_cnt[i] > 0)
+          CGX_NCCL(ncclSend(d_req + h.recv_off[i], (size_t)h.recv_cnt[i], ncclInt32, h.nbr[i],
+                            ctx->comm, s));
+        if (h.send_cnt[i] > 0)
+          CGX_NCCL(ncclRecv(d_inc + h.send_off[i], (size_t)h.send_cnt[i], ncclInt32, h.nbr[i],
+                            ctx->comm, s));
+      }
+      CGX_NCCL(ncclGroupEnd());
+    }
+    std::vector<int> inc((size_t)std::max<int64_t>(soff, 1));
+    CGX_HIP(hipMemcpyAsync(inc.data(), d_inc, inc.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(d_req);
+    (void)hipFree(d_inc);
+    for (int64_t i = 0; i < soff; ++i) {
+      const int64_t g = inc[i];
+      if (g < row_begin || g >= row_begin + n_local) {
+        cgx_free_host(ghosts);
+        cgx_csr_destroy(A);
+        set_error("rank %d was asked for row %lld it does not own", me, (long long)g);
+        return CGX_EINVAL;
+      }
+      inc[i] = (int)(g - row_begin);
+    }
+    const size_t es = dtype_size(dtype);
+    e = hipMalloc(&h.d_send_idx, (size_t)std::max<int64_t>(soff, 1) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h.d_send_buf, (size_t)std::max<int64_t>(soff, 1) * es);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h.d_send_idx, inc.data(), (size_t)soff * sizeof(int),
+                         hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      cgx_free_host(ghosts);
+      cgx_csr_destroy(A);
+      return hip_fail(e, "cgx_csr_create_dist(send plan)");
+    }
+  }
+  // 5. columns to local numbering, back to the device
+  rc = cgx_plan_remap(n_local, row_begin, nnz_local, hcol.data(), n_ghost, ghosts);
+  cgx_free_host(ghosts);
+  if (rc) {
+    cgx_csr_destroy(A);
+    return rc;
+  }
+  CGX_HIP(hipMemcpyAsync(d_col, hcol.data(), hcol.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  // 6. SpMV schedule over the local rows
+  int mx = 0;
+  std::vector<int> rb = build_row_blocks(hrp.data(), n_local, &mx);
+  CGX_HIP(hipMalloc(&A->d_rb, rb.size() * sizeof(int)));
+  CGX_HIP(hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  A->max_row_nnz = mx;
+  A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, (int)rb.size() - 1};
+  *out = A;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_halo_info(cgx_csr *A, int64_t *ghosts, int *neighbours) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  if (ghosts) *ghosts = A->halo.n_ghost;
+  if (neighbours) *neighbours = (int)A->halo.nbr.size();
+  return CGX_OK;
+}

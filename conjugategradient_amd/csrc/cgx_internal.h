@@ -1,0 +1,93 @@
+// cgx_internal.h — shared definitions between the HIP kernels
+// (cgx_kernels.hip) and the C-ABI host code (cgx_abi.cpp, cgx_dist.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace cgx {
+
+// ---- launch geometry --------------------------------------------------------
+constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
+constexpr int kTile = 2048;        // CSR entries staged in LDS per row block
+constexpr int kRowsPerBlock = 256; // max rows per row block (one per thread)
+constexpr int kMaxGrid = 2048;     // persistent grid cap: 256 CUs x 8 WGs
+constexpr int kMaxRed = 2;         // values reduced together (accuracy: 2)
+
+// ---- device-resident CG scalars (CG.hpp:280-289, made a ring) ----------------
+// Iteration k of a solve uses slot s = k % 4. Kernels of iteration k read
+// active[s] at entry and return at once when it is 0; the x/p-update kernel of
+// iteration k writes active[(s+1)%4] and rxr[(s+1)%4] (nobody in iteration k
+// reads those), which makes many iterations enqueue-able without a host sync
+// and keeps the reference's stop rule exact (CG.hpp:396-404,436).
+template <typename T> struct CgScalars {
+  T rxr[4];   // r.r at the start of the iteration in slot s
+  T pAp[4];   // value2 (CG.hpp:378)
+  T rr[4];    // value3 (CG.hpp:406)
+  T tol;      // acc (CG.hpp:286)
+  T pad_t;
+  int active[4];
+  long long bodies;  // loop bodies executed (the reference's counter + 1)
+  long long cap;     // max bodies: N+1 (CG.hpp:436) or a caller cap
+  int stopped;       // 0 running, 1 stop rule (tol / NaN), 2 cap reached
+  int pad_i;
+};
+
+// Grid-reduction workspace: one ticket + per-workgroup partials.
+template <typename T> struct RedWs {
+  unsigned int ticket;
+  unsigned int pad[3];
+  T partials[kMaxRed * kMaxGrid];
+};
+
+// ---- launchers (cgx_kernels.hip) --------------------------------------------
+struct CsrDev {
+  int64_t n, nnz;
+  const int *rowptr;
+  const int *col;
+  const void *val;
+  const int *rb;  // row-block starts, nrb + 1 entries
+  int nrb;
+};
+
+template <typename T> struct Launch {
+  static int grid_rows(int nrb);
+  static int grid_elems(int64_t n);
+  static hipError_t spmv(const CsrDev &A, const T *x, T *y, hipStream_t s);
+  static hipError_t cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
+                            CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
+                            hipStream_t s);
+  static hipError_t spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
+                             int slot, RedWs<T> *ws, hipStream_t s);
+  static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
+                             RedWs<T> *ws, hipStream_t s);
+  static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
+                              int slot, hipStream_t s);
+  static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,
+                            hipStream_t s);
+  static hipError_t axpby(int mode, int64_t n, const T *x, const T *y, const T *a,
+                          const T *b, T *res, hipStream_t s);
+  static hipError_t scalar_div(const T *num, const T *den, T *out, hipStream_t s);
+  static hipError_t fill(T *d, T v, int64_t n, hipStream_t s);
+  static hipError_t iota(T *d, int64_t n, double offset, hipStream_t s);
+  static hipError_t accuracy(const CsrDev &A, const T *b, const T *x, T *out2,
+                             RedWs<T> *ws, hipStream_t s);
+  static hipError_t poisson(int dim, int nx, int ny, int nz, int64_t row_begin,
+                            int64_t row_end, int *rowptr, int *col, T *val,
+                            hipStream_t s);
+  static hipError_t gather(const T *src, const int *idx, int64_t n, T *dst,
+                           hipStream_t s);
+};
+
+// axpby modes
+enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
+
+// host-side row-block schedule (cgx_abi.cpp)
+std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz);
+
+__host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, int64_t row);
+
+}  // namespace cgx

@@ -1,0 +1,111 @@
+// cgx_objects.h — definitions of the opaque C-ABI handles (cgx.h), shared by
+// cgx_abi.cpp (single-device engine) and cgx_dist.cpp (RCCL row partition).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/cgx.h"
+#include "cgx_internal.h"
+
+struct ncclComm;
+
+namespace cgx {
+
+void set_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);
+
+#define CGX_HIP(expr)                                   \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return ::cgx::hip_fail(e_, #expr); \
+  } while (0)
+
+#define CGX_REQUIRE(cond, code, ...)   \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::cgx::set_error(__VA_ARGS__);   \
+      return (code);                   \
+    }                                  \
+  } while (0)
+
+inline size_t dtype_size(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
+
+// Halo plan of a row-partitioned matrix (cgx_dist.cpp).
+struct Halo {
+  int64_t n_ghost = 0;
+  std::vector<int> nbr;            // neighbour ranks
+  std::vector<int64_t> recv_cnt;   // ghosts received from nbr[i] (contiguous)
+  std::vector<int64_t> recv_off;   // offset of that run inside the ghost area
+  std::vector<int64_t> send_cnt;   // entries sent to nbr[i]
+  std::vector<int64_t> send_off;   // offset inside send_idx / send_buf
+  int *d_send_idx = nullptr;       // local row indices to pack, all nbrs
+  void *d_send_buf = nullptr;      // packed values
+  int64_t send_total = 0;
+};
+
+}  // namespace cgx
+
+struct cgx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void *ws = nullptr;           // cgx::RedWs<double> (large enough for float)
+  void *scratch = nullptr;      // 2 doubles for accuracy() results
+  void *h_pinned = nullptr;     // pinned host staging (256 B)
+  // multi-GPU
+  ncclComm *comm = nullptr;
+  int rank = 0, world = 1;
+};
+
+struct cgx_csr {
+  cgx_ctx *ctx = nullptr;
+  cgx::CsrDev dev{};
+  int dtype = CGX_F64;
+  int *d_rb = nullptr;
+  int max_row_nnz = 0;
+  // distributed view
+  bool dist = false;
+  int64_t n_global = 0, row_begin = 0;
+  cgx::Halo halo;
+  void *d_ext = nullptr;  // scratch vector with ghost area (n + n_ghost)
+};
+
+struct cgx_cg {
+  cgx_ctx *ctx = nullptr;
+  cgx_csr *A = nullptr;
+  int dtype = CGX_F64;
+  int64_t n = 0;
+  void *r = nullptr, *p = nullptr, *Ap = nullptr;  // p, Ap: n + n_ghost
+  void *st = nullptr;   // cgx::CgScalars<T>
+  void *ws = nullptr;   // cgx::RedWs<T>
+  const void *b = nullptr;
+  void *x = nullptr;
+  int slot = 0;
+  bool begun = false;
+  int poll_every = 32;
+  bool use_graph = true;
+  // graph of `poll_every` iterations starting at slot 0
+  hipGraphExec_t graph = nullptr;
+  const void *graph_b = nullptr;
+  void *graph_x = nullptr;
+  int graph_iters = 0;
+  // kernel timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<std::pair<int, size_t>> ev_pending;  // (kernel id, event index)
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_calls[4] = {0, 0, 0, 0};
+};
+
+namespace cgx {
+// cgx_dist.cpp
+int dist_halo_exchange(cgx_csr *A, void *d_vec_ext, hipStream_t s);
+int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s);
+int dist_destroy_halo(cgx_csr *A);
+int dist_comm_destroy(cgx_ctx *ctx);
+}  // namespace cgx

@@ -1,0 +1,176 @@
+/*
+ * cgx.h — C ABI of libcgx.so, the MI355X (gfx950) conjugate-gradient engine.
+ *
+ * The reference (XeniaHerr/ConjugateGradient) has no FFI: its boundary is the
+ * header-only C++ template API in src/CG.hpp, src/VectorOperations.hpp and
+ * src/LinearAlgebraTypes.hpp. Our drop-in copies of those
+ * headers (include/CG.hpp, include/VectorOperations.hpp,
+ * include/LinearAlgebraTypes.hpp) are thin C++ over the entry points below;
+ * each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = CGX_OK, otherwise an error code; the
+ *     message is in cgx_last_error() (thread-local).
+ *   - Pointers named d_* are device pointers (hipMalloc'ed, e.g. by cgx_alloc);
+ *     h_* are host pointers. Sizes are element counts unless named *_bytes.
+ *   - dtype: CGX_F64 or CGX_F32 (the reference's DT template parameter).
+ *   - All kernels are asynchronous on the context's stream (the SYCL queue's
+ *     role, CG.hpp:590); functions documented as "blocking" drain it, as the
+ *     reference's executeQueue() does (CG.hpp:561-578).
+ *   - Indices are int32 (Matrix<DT> stores int columns/rows,
+ *     LinearAlgebraTypes.hpp:620-622).
+ */
+#ifndef CGX_H
+#define CGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CGX_OK = 0, CGX_EINVAL = 1, CGX_EHIP = 2, CGX_ENOMEM = 3, CGX_ESTATE = 4,
+       CGX_ENCCL = 5, CGX_EUNSUPPORTED = 6 };
+enum { CGX_F64 = 0, CGX_F32 = 1 };
+
+typedef struct cgx_ctx cgx_ctx; /* device + stream (+ optional RCCL comm)      */
+typedef struct cgx_csr cgx_csr; /* CSR matrix view + SpMV row-block schedule  */
+typedef struct cgx_cg cgx_cg;   /* fused CG solver state                      */
+
+/* ---- errors / version ---------------------------------------------------- */
+const char *cgx_last_error(void);
+const char *cgx_version(void);
+/* Number of visible HIP devices (0 when none; never fails on a CPU host). */
+int cgx_device_count(int *count);
+
+/* ---- context: replaces the sycl::queue (CG.hpp:61,70-77,590) -------------- */
+int cgx_create(int device, cgx_ctx **out);          /* CG::createCG :70-77   */
+int cgx_destroy(cgx_ctx *ctx);
+int cgx_sync(cgx_ctx *ctx);                          /* executeQueue :561-578 */
+int cgx_get_stream(cgx_ctx *ctx, void **hip_stream);
+int cgx_get_device(cgx_ctx *ctx, int *device);
+
+/* ---- memory: replaces sycl::malloc_device/free/copy/fill ------------------
+ * (LinearAlgebraTypes.hpp:43-49 Asycl_deleter, :109-119 Matrix::init,
+ *  :160-183 Vector::init_empty/init, :217-224 Scalar::init) */
+int cgx_alloc(cgx_ctx *ctx, size_t bytes, void **d_out);
+int cgx_free(cgx_ctx *ctx, void *d_ptr);
+int cgx_h2d(cgx_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);     /* blocking */
+int cgx_d2h(cgx_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);     /* blocking */
+int cgx_d2d(cgx_ctx *ctx, void *d_dst, const void *d_src, size_t bytes);     /* async    */
+int cgx_h2d_async(cgx_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int cgx_fill(cgx_ctx *ctx, int dtype, void *d_ptr, double value, size_t n);  /* async    */
+
+/* ---- CSR matrix (Matrix<DT>, LinearAlgebraTypes.hpp:57-132) ---------------
+ * The device arrays stay owned by the caller (the Matrix object's
+ * shared_ptrs); cgx_csr only adds the SpMV schedule. h_rowptr may be NULL (it
+ * is then read back from the device). */
+int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d_rowptr,
+                   const int *d_col, const void *d_val, int dtype,
+                   const int *h_rowptr, cgx_csr **out);
+int cgx_csr_destroy(cgx_csr *csr);
+int cgx_csr_info(cgx_csr *csr, int64_t *n, int64_t *nnz, int64_t *row_blocks,
+                 int *max_row_nnz);
+
+/* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
+ * Scalars are DEVICE pointers, as in the reference (Scalar<DT>::ptr()). */
+/* y = A x over all rows; `count` must equal A.N() (spmv :438-466, assert :444) */
+int cgx_spmv(cgx_ctx *ctx, cgx_csr *A, const void *d_x, void *d_y, int64_t count);
+/* *d_res += x.y  (dot_product_trivial :287-309: accumulates, Q4) */
+int cgx_dot_acc(cgx_ctx *ctx, int dtype, int64_t n, const void *d_x,
+                const void *d_y, void *d_res);
+/* *d_res += x.x  (norm :311-331; sum of squares, no sqrt) */
+int cgx_norm_acc(cgx_ctx *ctx, int dtype, int64_t n, const void *d_x, void *d_res);
+/* res = x + (*d_b) y (sapbx :410-428), res = x - (*d_b) y (sambx :380-397),
+ * res = (*d_a) x + (*d_b) y (saxpby :349-367). res may alias x or y. */
+int cgx_sapbx(cgx_ctx *ctx, int dtype, int64_t n, const void *d_x,
+              const void *d_y, const void *d_b, void *d_res);
+int cgx_sambx(cgx_ctx *ctx, int dtype, int64_t n, const void *d_x,
+              const void *d_y, const void *d_b, void *d_res);
+int cgx_saxpby(cgx_ctx *ctx, int dtype, int64_t n, const void *d_x,
+               const void *d_y, const void *d_a, const void *d_b, void *d_res);
+/* Device scalar helper: *d_out = *d_num / *d_den (CG.hpp:385-386, :414). */
+int cgx_scalar_div(cgx_ctx *ctx, int dtype, const void *d_num, const void *d_den,
+                   void *d_out);
+
+/* ---- fused CG: CG<DT>::solve (CG.hpp:255-454) -----------------------------
+ * Per iteration three kernels (SpMV+p.Ap, r-update+r.r, x/p-update), device-
+ * resident scalars and stop flag; the host polls every few iterations instead
+ * of draining the queue every iteration (CG.hpp:425). Iteration semantics are
+ * the reference's (Q5): the stop test uses the r.r at the START of the body
+ * after the body's x update, NaN stops, at most A.N()+1 bodies. */
+int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out);
+int cgx_cg_destroy(cgx_cg *cg);
+/* Blocking. d_x holds the initial guess (zero it for the reference default)
+ * and receives the result. max_bodies < 0 keeps the reference cap N+1;
+ * otherwise the cap is min(N+1, max_bodies). */
+int cgx_cg_solve(cgx_cg *cg, const void *d_b, void *d_x, double tol,
+                 int64_t max_bodies, int64_t *bodies_out, double *rxr_out);
+/* Split form used by benchmarks: init (r = b - A x, p = r, rxr = r.r) then
+ * run up to `bodies` more loop bodies (stops early on the stop rule). */
+int cgx_cg_begin(cgx_cg *cg, const void *d_b, void *d_x, double tol,
+                 int64_t max_bodies);
+int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int *stopped);
+/* Per-kernel device time, accumulated with HIP events on the solver stream
+ * while enabled: avg_ms[0..3] = init, spmv_dot, update_r, update_xp;
+ * calls[0..3] = launches timed. */
+int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable);
+int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
+/* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
+int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
+
+/* CG::accuracy (CG.hpp:463-515): blocking; |sum (b-Ax)^2 / sum x^2|. */
+int cgx_accuracy(cgx_ctx *ctx, cgx_csr *A, const void *d_b, const void *d_x,
+                 double *out);
+
+/* ---- synthetic inputs ---------------------------------------
+ * Dirichlet Poisson CSR generated on the device (dim 2: 5-point, dim 3:
+ * 7-point; lexicographic, x fastest; columns ascending; diag 2*dim, off -1).
+ * Rows [row_begin, row_end) of the global matrix; column indices global. */
+int64_t cgx_poisson_nnz(int dim, int nx, int ny, int nz, int64_t row_begin,
+                        int64_t row_end);
+int cgx_poisson_fill(cgx_ctx *ctx, int dtype, int dim, int nx, int ny, int nz,
+                     int64_t row_begin, int64_t row_end, int *d_rowptr,
+                     int *d_col, void *d_val);
+/* b_i = i + 1 + offset (Tester.cpp:29-30) */
+int cgx_iota(cgx_ctx *ctx, int dtype, void *d_b, int64_t n, double offset);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI --------
+ * Rows are partitioned in contiguous blocks; p's ghost entries are exchanged
+ * each iteration with ncclSend/ncclRecv and the two dots are all-reduced. */
+int cgx_nccl_unique_id(char *id_out, size_t len);            /* len >= 128 */
+int cgx_dist_init(cgx_ctx *ctx, int rank, int world, const char *id, size_t len);
+int cgx_dist_rank(cgx_ctx *ctx, int *rank, int *world);
+/* Local block of a globally row-partitioned matrix: rows
+ * [row_begin, row_begin + n_local) with GLOBAL column indices (device arrays,
+ * caller-owned, d_col is rewritten in place to local/ghost numbering).
+ * n_global is the global dimension. Collective over the communicator. */
+int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_begin,
+                        int64_t n_local, int64_t nnz_local, const int *d_rowptr,
+                        int *d_col, const void *d_val, int dtype, cgx_csr **out);
+/* ghost entries this rank receives per iteration */
+int cgx_csr_halo_info(cgx_csr *csr, int64_t *ghosts, int *neighbours);
+/* Reduce a host double over ranks (sum); utility for tests. */
+int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value);
+
+/* ---- host-only helpers (no device needed; the CPU test-suite drives them) --
+ * Halo plan of rows [row_begin, row_begin + n_local) whose global column
+ * indices are `col`: sorted distinct off-block columns (*ghosts, malloc'ed,
+ * release with cgx_free_host) and per-rank receive counts (recv_cnt[world]);
+ * begins/counts give every rank's row range (contiguous, ordered by rank). */
+int cgx_plan_ghosts(int64_t n_local, int64_t row_begin, int64_t nnz, const int *col,
+                    int world, const int64_t *begins, const int64_t *counts,
+                    int64_t *n_ghost, int64_t **ghosts, int64_t *recv_cnt);
+/* Global -> local column numbering (own rows, then ghosts in list order). */
+int cgx_plan_remap(int64_t n_local, int64_t row_begin, int64_t nnz, int *col,
+                   int64_t n_ghost, const int64_t *ghosts);
+/* The SpMV row-block schedule cgx_csr_create builds (for tests). */
+int cgx_row_blocks(const int *h_rowptr, int64_t n, int64_t *nrb, int **rb,
+                   int *max_row_nnz);
+void cgx_free_host(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGX_H */
