@@ -90,6 +90,7 @@ _SIGS = {
                                C.POINTER(C.POINTER(_i64)), _vp]),
     "cgx_plan_remap": (_i32, [_i64, _i64, _i64, _vp, _i64, _vp]),
     "cgx_free_host": (None, [_vp]),
+    "cgx_tune_spmv": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, C.POINTER(_dbl)]),
     "cgx_row_blocks": (_i32, [_vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i32)),
                               C.POINTER(_i32)]),
 }

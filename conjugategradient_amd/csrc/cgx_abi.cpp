@@ -44,14 +44,14 @@ std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz
   while (row < n) {
     const int64_t start = row;
     int len = rowptr[row + 1] - rowptr[row];
-    if (len > kTile) {  // a long row gets a workgroup of its own
+    if (len > kTileCap) {  // a long row gets a workgroup of its own
       mx = std::max(mx, len);
       ++row;
     } else {
       int64_t acc = 0;
       while (row < n && row - start < kRowsPerBlock) {
         len = rowptr[row + 1] - rowptr[row];
-        if (acc + len > kTile) break;
+        if (acc + len > kTileCap) break;
         acc += len;
         mx = std::max(mx, len);
         ++row;
@@ -379,11 +379,14 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
               (long long)nnz);
   int mx = 0;
   std::vector<int> rb = build_row_blocks(h_rowptr, n, &mx);
+  const size_t nrb1 = rb.size();
+  rb.resize(2 * nrb1);  // second half: entry offset of each row block
+  for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = h_rowptr[rb[i]];
   auto *A = new cgx_csr();
   A->ctx = ctx;
   A->dtype = dtype;
   A->max_row_nnz = mx;
-  A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, (int)rb.size() - 1};
+  A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, nullptr, (int)nrb1 - 1};
   hipError_t e = hipMalloc(&A->d_rb, rb.size() * sizeof(int));
   if (e == hipSuccess)
     e = hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -394,6 +397,7 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
     return hip_fail(e, "cgx_csr_create");
   }
   A->dev.rb = A->d_rb;
+  A->dev.rbk = A->d_rb + nrb1;
   A->n_global = n;
   *out = A;
   return CGX_OK;
@@ -817,5 +821,47 @@ extern "C" int cgx_iota(cgx_ctx *ctx, int dtype, void *d_b, int64_t n, double of
   DeviceGuard g(ctx->device);
   if (dtype == CGX_F32) CGX_HIP(Launch<float>::iota((float *)d_b, n, offset, ctx->stream));
   else CGX_HIP(Launch<double>::iota((double *)d_b, n, offset, ctx->stream));
+  return CGX_OK;
+}
+
+// ===========================================================================
+// diagnostics: time one SpMV(+p.Ap) variant (bits: cgx_kernels.hip spmv_rows)
+// ===========================================================================
+extern "C" int cgx_tune_spmv(cgx_ctx *ctx, cgx_csr *A, int variant, const void *x, void *y,
+                             int iters, double *avg_ms) {
+  CGX_REQUIRE(ctx && A && x && y && avg_ms && iters > 0, CGX_EINVAL, "bad argument");
+  CGX_REQUIRE(!A->dist, CGX_EUNSUPPORTED, "tuning runs on a single-device matrix");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  void *st = nullptr;
+  CGX_HIP(hipMalloc(&st, sizeof(CgScalars<double>)));
+  CGX_HIP(hipMemsetAsync(st, 0, sizeof(CgScalars<double>), s));
+  const int one = 1;
+  const size_t off = A->dtype == CGX_F32 ? offsetof(CgScalars<float>, active)
+                                         : offsetof(CgScalars<double>, active);
+  CGX_HIP(hipMemcpyAsync((char *)st + off, &one, sizeof(int), hipMemcpyHostToDevice, s));
+  hipEvent_t e0, e1;
+  CGX_HIP(hipEventCreate(&e0));
+  CGX_HIP(hipEventCreate(&e1));
+  hipError_t e = hipSuccess;
+  for (int i = 0; i <= iters && e == hipSuccess; ++i) {  // first launch = warm-up
+    if (i == 1) e = hipEventRecord(e0, s);
+    if (e != hipSuccess) break;
+    if (A->dtype == CGX_F32)
+      e = Launch<float>::spmv_dot_variant(variant, A->dev, (const float *)x, (float *)y,
+                                          (CgScalars<float> *)st, (RedWs<float> *)ctx->ws, s);
+    else
+      e = Launch<double>::spmv_dot_variant(variant, A->dev, (const double *)x, (double *)y,
+                                           (CgScalars<double> *)st, (RedWs<double> *)ctx->ws, s);
+  }
+  if (e == hipSuccess) e = hipEventRecord(e1, s);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(st);
+  CGX_HIP(e);
+  *avg_ms = ms / iters;
   return CGX_OK;
 }

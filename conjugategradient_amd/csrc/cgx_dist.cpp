@@ -348,11 +348,15 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   // 6. SpMV schedule over the local rows
   int mx = 0;
   std::vector<int> rb = build_row_blocks(hrp.data(), n_local, &mx);
+  const size_t nrb1 = rb.size();
+  rb.resize(2 * nrb1);
+  for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = hrp[rb[i]];
   CGX_HIP(hipMalloc(&A->d_rb, rb.size() * sizeof(int)));
   CGX_HIP(hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s));
   CGX_HIP(hipStreamSynchronize(s));
   A->max_row_nnz = mx;
-  A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, (int)rb.size() - 1};
+  A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, A->d_rb + nrb1,
+                  (int)nrb1 - 1};
   *out = A;
   return CGX_OK;
 }

@@ -13,6 +13,7 @@ namespace cgx {
 // ---- launch geometry --------------------------------------------------------
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 constexpr int kTile = 2048;        // CSR entries staged in LDS per row block
+constexpr int kTileCap = kTile - 2; // entries a row block may hold (paired loads)
 constexpr int kRowsPerBlock = 256; // max rows per row block (one per thread)
 constexpr int kMaxGrid = 2048;     // persistent grid cap: 256 CUs x 8 WGs
 constexpr int kMaxRed = 2;         // values reduced together (accuracy: 2)
@@ -49,7 +50,8 @@ struct CsrDev {
   const int *rowptr;
   const int *col;
   const void *val;
-  const int *rb;  // row-block starts, nrb + 1 entries
+  const int *rb;   // row-block starts, nrb + 1 entries
+  const int *rbk;  // rowptr[rb[i]], nrb + 1 entries
   int nrb;
 };
 
@@ -62,6 +64,8 @@ template <typename T> struct Launch {
                             hipStream_t s);
   static hipError_t spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
                              int slot, RedWs<T> *ws, hipStream_t s);
+  static hipError_t spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
+                                     CgScalars<T> *st, RedWs<T> *ws, hipStream_t s);
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s);
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,

@@ -132,52 +132,120 @@ __device__ __forceinline__ int logical_block() {
 struct CsrArgs {
   const int *__restrict__ rowptr;
   const int *__restrict__ col;
-  const int *__restrict__ rb;
+  const int *__restrict__ rb;   // first row of each row block (nrb + 1)
+  const int *__restrict__ rbk;  // rowptr[rb[i]]: first entry of each row block
   int nrb;
 };
 
 template <typename T> struct SpmvLds {
-  T prod[kTile];
+  T prod[kTile + 2];  // + 2 scratch slots for branch-free out-of-range stores
   int rp[kRowsPerBlock + 1];
   T red[4 * kMaxRed];
   int flag;
 };
 
-template <typename T, class Epi>
+// Variant bits of the SpMV row loop (A/B-tested with cgx_tune_spmv):
+//   1  XCD-contiguous work split: the blockIdx%8 group g walks row blocks
+//      [g*nrb/8, (g+1)*nrb/8), so the p rows a block gathers were mostly just
+//      fetched into the same XCD's L2 by its neighbours;
+//   2  non-temporal loads for the once-read val/col streams (keep L2 for p);
+//   4  paired loads: val as 16-B (f64) pairs and col as 8-B pairs from an
+//      aligned base (the schedule caps a tile at kTile-2 entries so 4 passes
+//      of 256 pairs always cover it).
+template <typename T> struct PairOf;
+template <> struct PairOf<double> { typedef double V __attribute__((ext_vector_type(2))); };
+template <> struct PairOf<float> { typedef float V __attribute__((ext_vector_type(2))); };
+typedef int Int2 __attribute__((ext_vector_type(2)));
+
+template <bool NT, typename P> __device__ __forceinline__ P ldg(const P *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int V>
+__device__ __forceinline__ void work_range(int nrb, int &first, int &step, int &end) {
+  const int G = gridDim.x;
+  if ((V & 1) && (G & 7) == 0) {
+    const int g = blockIdx.x & 7, per = G >> 3;
+    first = (int)(((int64_t)nrb * g) >> 3) + (blockIdx.x >> 3);
+    end = (int)(((int64_t)nrb * (g + 1)) >> 3);
+    step = per;
+  } else {
+    first = logical_block();
+    step = G;
+    end = nrb;
+  }
+}
+
+template <typename T, int V, class Epi>
 __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict__ val,
                                           const T *__restrict__ x, Epi &epi,
                                           SpmvLds<T> &sm) {
-  constexpr int U = kTile / kBlock;
+  constexpr bool NT = (V & 2) != 0;
+  constexpr bool PAIRS = (V & 4) != 0;
   const int t = threadIdx.x;
-  for (int b = logical_block(); b < A.nrb; b += gridDim.x) {
+  int first, step, end;
+  work_range<V>(A.nrb, first, step, end);
+  for (int b = first; b < end; b += step) {
     const int r0 = A.rb[b], r1 = A.rb[b + 1];
     const int nrows = r1 - r0;
     for (int i = t; i <= nrows; i += kBlock) sm.rp[i] = A.rowptr[r0 + i];
     __syncthreads();
     const int k0 = sm.rp[0];
     const int cnt = sm.rp[nrows] - k0;
-    if (cnt <= kTile) {
+    if (cnt <= kTileCap) {
       if (cnt > 0) {
-        T v[U];
-        int c[U];
+        if constexpr (PAIRS) {
+          using PV = typename PairOf<T>::V;
+          constexpr int U = kTile / (2 * kBlock);
+          const int ka = k0 & ~1;
+          const int npairs = (k0 + cnt - ka + 1) >> 1;
+          const PV *v2 = reinterpret_cast<const PV *>(val + ka);
+          const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
+          PV v[U];
+          Int2 c[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int k = min(t + u * kBlock, cnt - 1);
-          v[u] = val[k0 + k];
-          c[u] = A.col[k0 + k];
-        }
-        T g[U];
+          for (int u = 0; u < U; ++u) {
+            const int j = min(t + u * kBlock, npairs - 1);
+            v[u] = ldg<NT>(v2 + j);
+            c[u] = ldg<NT>(c2 + j);
+          }
+          T g0[U], g1[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) g[u] = x[c[u]];
+          for (int u = 0; u < U; ++u) {
+            g0[u] = x[c[u].x];
+            g1[u] = x[c[u].y];
+          }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int k = t + u * kBlock;
-          if (k < cnt) sm.prod[k] = v[u] * g[u];
+          for (int u = 0; u < U; ++u) {
+            const int pos = 2 * (t + u * kBlock) + ka - k0;
+            if (pos >= 0 && pos < cnt) sm.prod[pos] = v[u].x * g0[u];
+            if (pos + 1 >= 0 && pos + 1 < cnt) sm.prod[pos + 1] = v[u].y * g1[u];
+          }
+        } else {
+          constexpr int U = kTile / kBlock;
+          T v[U];
+          int c[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = min(t + u * kBlock, cnt - 1);
+            v[u] = ldg<NT>(val + k0 + k);
+            c[u] = ldg<NT>(A.col + k0 + k);
+          }
+          T g[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) g[u] = x[c[u]];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = t + u * kBlock;
+            if (k < cnt) sm.prod[k] = v[u] * g[u];
+          }
         }
       }
       __syncthreads();
       if (t < nrows) {
         const int a = sm.rp[t] - k0, e = sm.rp[t + 1] - k0;
+        epi.pre(r0 + t);
         T s = T(0);
         for (int j = a; j < e; ++j) s += sm.prod[j];
         epi.row(r0 + t, s);
@@ -188,32 +256,145 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
       T s[1] = {T(0)};
       for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x[A.col[k0 + k]];
       block_sum<T, 1>(s, sm.red);
-      if (t == 0) epi.row(r0, s[0]);
+      if (t == 0) {
+        epi.pre(r0);
+        epi.row(r0, s[0]);
+      }
       __syncthreads();
     }
   }
 }
 
+// Software-pipelined form (variant bit 8, paired loads only): while a block
+// gathers p and sums its rows, the val/col pairs of the block it processes
+// next are already in flight. Every load is issued unconditionally (clamped
+// to valid addresses) so the compiler's in-order vmcnt bookkeeping can wait
+// for the current block's gathers without draining the prefetch.
+template <typename T, int V, class Epi>
+__device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__restrict__ val,
+                                               const T *__restrict__ x, Epi &epi,
+                                               SpmvLds<T> &sm) {
+  constexpr bool NT = (V & 2) != 0;
+  using PV = typename PairOf<T>::V;
+  constexpr int U = kTile / (2 * kBlock);
+  const int t = threadIdx.x;
+  int b, step, end;
+  work_range<V>(A.nrb, b, step, end);
+  if (b >= end) return;
+  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  PV v[U];
+  Int2 c[U];
+  auto issue = [&](int kk0, int kk1, PV(&vv)[U], Int2(&cc)[U]) {
+    const bool ok = kk1 > kk0;  // empty blocks read pairs [0, 1] (nnz >= 2)
+    const int ka = ok ? (kk0 & ~1) : 0;
+    const int np = ok ? ((kk1 - ka + 1) >> 1) : 1;
+    const PV *v2 = reinterpret_cast<const PV *>(val + ka);
+    const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(t + u * kBlock, np - 1);
+      vv[u] = ldg<NT>(v2 + j);
+      cc[u] = ldg<NT>(c2 + j);
+    }
+  };
+  issue(k0, k1, v, c);
+  for (;;) {
+    const int nb = b + step;
+    const bool has_next = nb < end;
+    const int nbb = has_next ? nb : b;
+    const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
+    const int nrows = r1 - r0, cnt = k1 - k0;
+    const int tr = min(t, max(nrows - 1, 0));
+    const int a = A.rowptr[r0 + tr] - k0, e = A.rowptr[r0 + tr + 1] - k0;
+    epi.pre(r0 + tr);
+    T g0[U], g1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g0[u] = x[c[u].x];
+      g1[u] = x[c[u].y];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    PV vn[U];
+    Int2 cn[U];
+    issue(nk0, nk1, vn, cn);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      // branch-free: lanes outside [0, cnt) store into the scratch slots
+      const int ka = k0 & ~1;
+      const int lim = min(cnt, kTileCap);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pos = 2 * (t + u * kBlock) + ka - k0;
+        const int q0 = (pos >= 0 && pos < lim) ? pos : kTile;
+        const int q1 = (pos + 1 >= 0 && pos + 1 < lim) ? pos + 1 : kTile + 1;
+        sm.prod[q0] = v[u].x * g0[u];
+        sm.prod[q1] = v[u].y * g1[u];
+      }
+    }
+    if (cnt <= kTileCap) {
+      __syncthreads();
+      if (t < nrows) {
+        T s = T(0);
+        for (int j = a; j < e; ++j) s += sm.prod[j];
+        epi.row(r0 + t, s);
+      }
+      __syncthreads();
+    } else {
+      // one row longer than a tile
+      __syncthreads();
+      T s[1] = {T(0)};
+      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x[A.col[k0 + k]];
+      block_sum<T, 1>(s, sm.red);
+      if (t == 0) epi.row(r0, s[0]);
+      __syncthreads();
+    }
+    if (!has_next) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = vn[u];
+      c[u] = cn[u];
+    }
+    b = nb;
+    r0 = nr0;
+    r1 = nr1;
+    k0 = nk0;
+    k1 = nk1;
+  }
+}
+
+template <typename T, int V, class Epi>
+__device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
+                                         const T *__restrict__ x, Epi &epi, SpmvLds<T> &sm) {
+  if constexpr ((V & 8) != 0) spmv_rows_pipe<T, V, Epi>(A, val, x, epi, sm);
+  else spmv_rows<T, V, Epi>(A, val, x, epi, sm);
+}
+
+// Row epilogues: pre(i) loads the row's own operands early (the pipelined
+// loop issues it before the next block's prefetch, so waiting on it never
+// waits on the prefetch); row(i, s) consumes the row sum.
 template <typename T> struct EpiStore {
   T *__restrict__ y;
+  __device__ __forceinline__ void pre(int) {}
   __device__ __forceinline__ void row(int i, T s) { y[i] = s; }
 };
 template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
   T *__restrict__ Ap;
   const T *__restrict__ p;
-  T acc;
+  T acc, pv;
+  __device__ __forceinline__ void pre(int i) { pv = p[i]; }
   __device__ __forceinline__ void row(int i, T s) {
     Ap[i] = s;
-    acc += s * p[i];
+    acc += s * pv;
   }
 };
 template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
   const T *__restrict__ b;
   T *__restrict__ r;
   T *__restrict__ p;
-  T acc;
+  T acc, bv;
+  __device__ __forceinline__ void pre(int i) { bv = b[i]; }
   __device__ __forceinline__ void row(int i, T s) {
-    const T ri = b[i] - s;
+    const T ri = bv - s;
     r[i] = ri;
     p[i] = ri;
     acc += ri * ri;
@@ -222,31 +403,35 @@ template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
 template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
-  T acc0, acc1;
+  T acc0, acc1, bv, xv;
+  __device__ __forceinline__ void pre(int i) {
+    bv = b[i];
+    xv = x[i];
+  }
   __device__ __forceinline__ void row(int i, T s) {
-    const T a = b[i] - s;
+    const T a = bv - s;
     acc0 += a * a;
-    acc1 += x[i] * x[i];
+    acc1 += xv * xv;
   }
 };
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_spmv(CsrArgs A, const T *__restrict__ val,
                                                  const T *__restrict__ x, T *__restrict__ y) {
   __shared__ SpmvLds<T> sm;
   EpiStore<T> e{y};
-  spmv_rows(A, val, x, e, sm);
+  spmv_any<T, V>(A, val, x, e, sm);
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restrict__ val,
                                                     const T *__restrict__ x,
                                                     const T *__restrict__ b, T *__restrict__ r,
                                                     T *__restrict__ p, CgScalars<T> *st,
                                                     RedWs<T> *ws, T tol, long long cap) {
   __shared__ SpmvLds<T> sm;
-  EpiInit<T> e{b, r, p, T(0)};
-  spmv_rows(A, val, x, e, sm);
+  EpiInit<T> e{b, r, p, T(0), T(0)};
+  spmv_any<T, V>(A, val, x, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
     st->rxr[0] = v[0];
@@ -260,27 +445,27 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restrict__ val,
                                                      const T *__restrict__ p,
                                                      T *__restrict__ Ap, CgScalars<T> *st,
                                                      int slot, RedWs<T> *ws) {
   if (!st->active[slot]) return;
   __shared__ SpmvLds<T> sm;
-  EpiDot<T> e{Ap, p, T(0)};
-  spmv_rows(A, val, p, e, sm);
+  EpiDot<T> e{Ap, p, T(0), T(0)};
+  spmv_any<T, V>(A, val, p, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) st->pAp[slot] = v[0];
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_accuracy(CsrArgs A, const T *__restrict__ val,
                                                      const T *__restrict__ b,
                                                      const T *__restrict__ x, T *out2,
                                                      RedWs<T> *ws) {
   __shared__ SpmvLds<T> sm;
-  EpiAccuracy<T> e{b, x, T(0), T(0)};
-  spmv_rows(A, val, x, e, sm);
+  EpiAccuracy<T> e{b, x, T(0), T(0), T(0), T(0)};
+  spmv_any<T, V>(A, val, x, e, sm);
   T v[2] = {e.acc0, e.acc1};
   if (grid_reduce<T, 2>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
     out2[0] = v[0];
@@ -504,7 +689,7 @@ inline int elem_grid(int64_t n, int per_thread) {
   return (int)g;
 }
 
-inline CsrArgs args(const CsrDev &A) { return CsrArgs{A.rowptr, A.col, A.rb, A.nrb}; }
+inline CsrArgs args(const CsrDev &A) { return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb}; }
 
 }  // namespace
 
@@ -535,21 +720,68 @@ template <typename T> int Launch<T>::grid_elems(int64_t n) { return elem_grid(n,
     return hipGetLastError();                                                      \
   } while (0)
 
+// SpMV variant used in production (bits: see spmv_rows / spmv_rows_pipe),
+// chosen with cgx_tune_spmv on MI355X (profiles/r01_tune_spmv.log):
+// pipelined + paired + XCD split, with non-temporal val/col loads only when
+// the matrix outgrows the 256 MiB Infinity Cache (a cache-resident matrix is
+// re-read every iteration, nt loads would throw that reuse away). Without
+// 16-B aligned val / 8-B aligned col the paired and pipelined bits drop.
+constexpr int kSpmvV = -1;
+constexpr int64_t kNtMinBytes = int64_t(256) << 20;
+
+template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
+  if (v < 0) v = (A.nnz * int64_t(sizeof(T) + sizeof(int)) >= kNtMinBytes) ? 15 : 13;
+  v &= 15;
+  if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2) v &= ~12;
+  if ((v & 8) && !(v & 4)) v &= ~8;  // the pipelined loop uses paired loads
+  return v;
+}
+
+#define CGX_LAUNCH_V(KERNEL, VV, ...)                                          \
+  do {                                                                         \
+    hipLaunchKernelGGL((KERNEL<T, VV>), dim3(grid_rows(A.nrb)), dim3(kBlock), 0, s, \
+                       __VA_ARGS__);                                           \
+    return hipGetLastError();                                                  \
+  } while (0)
+
+#define CGX_SPMV_SWITCH(v, KERNEL, ...)                                        \
+  switch (v) {                                                                 \
+    case 0: CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);                              \
+    case 1: CGX_LAUNCH_V(KERNEL, 1, __VA_ARGS__);                              \
+    case 2: CGX_LAUNCH_V(KERNEL, 2, __VA_ARGS__);                              \
+    case 3: CGX_LAUNCH_V(KERNEL, 3, __VA_ARGS__);                              \
+    case 4: CGX_LAUNCH_V(KERNEL, 4, __VA_ARGS__);                              \
+    case 5: CGX_LAUNCH_V(KERNEL, 5, __VA_ARGS__);                              \
+    case 6: CGX_LAUNCH_V(KERNEL, 6, __VA_ARGS__);                              \
+    case 7: CGX_LAUNCH_V(KERNEL, 7, __VA_ARGS__);                              \
+    case 12: CGX_LAUNCH_V(KERNEL, 12, __VA_ARGS__);                            \
+    case 13: CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);                            \
+    case 14: CGX_LAUNCH_V(KERNEL, 14, __VA_ARGS__);                            \
+    default: CGX_LAUNCH_V(KERNEL, 15, __VA_ARGS__);                            \
+  }
+
 template <typename T>
 hipError_t Launch<T>::spmv(const CsrDev &A, const T *x, T *y, hipStream_t s) {
-  CGX_LAUNCH(k_spmv<T>, grid_rows(A.nrb), args(A), (const T *)A.val, x, y);
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv, args(A), (const T *)A.val, x, y);
 }
 template <typename T>
 hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                               CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
                               hipStream_t s) {
-  CGX_LAUNCH(k_cg_init<T>, grid_rows(A.nrb), args(A), (const T *)A.val, x, b, r, p, st, ws,
-             tol, cap);
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws,
+                  tol, cap);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
                                int slot, RedWs<T> *ws, hipStream_t s) {
-  CGX_LAUNCH(k_spmv_dot<T>, grid_rows(A.nrb), args(A), (const T *)A.val, p, Ap, st, slot, ws);
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, slot,
+                  ws);
+}
+template <typename T>
+hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
+                                       CgScalars<T> *st, RedWs<T> *ws, hipStream_t s) {
+  CGX_SPMV_SWITCH(spmv_variant<T>(A, v), k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0,
+                  ws);
 }
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
@@ -586,7 +818,7 @@ hipError_t Launch<T>::iota(T *d, int64_t n, double offset, hipStream_t s) {
 template <typename T>
 hipError_t Launch<T>::accuracy(const CsrDev &A, const T *b, const T *x, T *out2,
                                RedWs<T> *ws, hipStream_t s) {
-  CGX_LAUNCH(k_accuracy<T>, grid_rows(A.nrb), args(A), (const T *)A.val, b, x, out2, ws);
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_accuracy, args(A), (const T *)A.val, b, x, out2, ws);
 }
 template <typename T>
 hipError_t Launch<T>::poisson(int dim, int nx, int ny, int nz, int64_t row_begin,

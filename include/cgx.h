@@ -170,6 +170,13 @@ int cgx_row_blocks(const int *h_rowptr, int64_t n, int64_t *nrb, int **rb,
                    int *max_row_nnz);
 void cgx_free_host(void *p);
 
+/* ---- diagnostics ------------------------------------------------------------
+ * Average device time (ms) of `iters` launches of the SpMV + p.Ap kernel in
+ * variant `variant` (bit 1: XCD-contiguous split, 2: non-temporal val/col
+ * loads, 4: paired 16-B/8-B loads), y = A x. For A/B tuning on one device. */
+int cgx_tune_spmv(cgx_ctx *ctx, cgx_csr *A, int variant, const void *d_x, void *d_y,
+                  int iters, double *avg_ms);
+
 #ifdef __cplusplus
 }
 #endif

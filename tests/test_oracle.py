@@ -1,0 +1,132 @@
+"""Pin the oracle (oracle/cg_oracle.c, the CPU restatement of the reference)
+before trusting it (CPU only).
+
+* Loader: bit-exact against the reference's own test/mm_reader.cpp, compiled
+  unmodified into oracle/_ref/libmmref.so, on the golden .mtx files including
+  the quirk cases Q1-Q3.
+* CG: the loop-body counts and accuracy() the survey recorded from the
+  reference itself: 103 / 2.52e-30 (16^2, 1e-24), 972 /
+  2.136e-29 (128^2, 1e-24), 479 (128^2, 1e-8), 152 / 76 (16^3); and, for the
+  probe's FMA build (-O3 -march=native), 972 / 2.160e-29 and 686 (64^3).
+* Independent check: x against a sparse direct solve (scipy).
+"""
+import glob
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.util import rel
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("dim,n,tol,iters,acc", [
+    (2, 16, 1e-24, 103, 2.52e-30),
+    (2, 128, 1e-24, 972, 2.136e-29),
+    (2, 128, 1e-8, 479, None),
+    (3, 16, 1e-24, 152, None),
+    (3, 16, 1e-8, 76, None),
+])
+def test_oracle_reproduces_recorded_reference_outputs(oracle, dim, n, tol, iters, acc):
+    rp, cl, vl = oracle.poisson(dim, n, n, n)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    x, res = oracle.cg_solve(rp, cl, vl, b, tol)
+    assert res.iterations == iters
+    if acc is not None:
+        assert oracle.accuracy(rp, cl, vl, b, x) == pytest.approx(acc, rel=2e-3)
+
+
+def test_oracle_fma_build_reproduces_probe(oracle, tmp_path):
+    """The survey's 64^3 count (686) and its -march=native 128^2 accuracy
+    (2.160e-29) come from an FMA-contracting build; the same source built the
+    same way reproduces both."""
+    so = str(tmp_path / "liboracle_fma.so")
+    src = os.path.join(os.path.dirname(oracle.LIB_PATH), "cg_oracle.c")
+    subprocess.run(["gcc", "-O3", "-march=native", "-ffp-contract=fast", "-fopenmp", "-fPIC",
+                    "-shared", "-o", so, src, "-lm"], check=True)
+    import ctypes as C
+
+    from oracle.oracle import CgResult
+    L = C.CDLL(so)
+    L.orc_cg_solve.argtypes = [C.c_int64] + [C.c_void_p] * 5 + [C.c_int, C.c_double, C.c_int64,
+                                                                C.POINTER(CgResult)]
+    L.orc_accuracy.argtypes = [C.c_int64] + [C.c_void_p] * 5
+    L.orc_accuracy.restype = C.c_double
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    for dim, n, want_it, want_acc in [(2, 128, 972, 2.160e-29), (3, 64, 686, None)]:
+        rp, cl, vl = oracle.poisson(dim, n, n, n)
+        N = len(rp) - 1
+        b = np.arange(1, N + 1, dtype=np.float64)
+        x = np.zeros(N)
+        r = CgResult()
+        L.orc_cg_solve(N, p(rp), p(cl), p(vl), p(b), p(x), 0, 1e-24, -1, C.byref(r))
+        assert r.iterations == want_it
+        if want_acc:
+            acc = L.orc_accuracy(N, p(rp), p(cl), p(vl), p(b), p(x))
+            assert acc == pytest.approx(want_acc, rel=2e-3)
+
+
+def test_oracle_against_direct_solve(oracle):
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+
+    rp, cl, vl = oracle.poisson(2, 128, 128, 1)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)
+    x, _ = oracle.cg_solve(rp, cl, vl, b, 1e-24)
+    xd = spl.spsolve(sp.csr_matrix((vl, cl, rp), shape=(n, n)).tocsc(), b)
+    assert rel(x, xd) < 1e-12
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "*.mtx"))))
+def test_loader_matches_reference_golden(oracle, path):
+    name = os.path.splitext(os.path.basename(path))[0]
+    g = np.load(os.path.join(GOLD, f"loader_{name}.npz"))
+    got = oracle.read_mtx(path)
+    for a, k in zip(got, ("rowptr", "col", "val")):
+        np.testing.assert_array_equal(a, g[k])
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "*.mtx"))))
+def test_loader_matches_reference_build(oracle, path):
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    ref = oracle.ref_read_mtx(path)
+    got = oracle.read_mtx(path)
+    for a, r in zip(got, ref):
+        np.testing.assert_array_equal(a, r)
+
+
+@pytest.mark.parametrize("name", ["poisson2d_16", "poisson2d_128", "poisson3d_16"])
+def test_oracle_matches_cg_golden(oracle, name):
+    g = np.load(os.path.join(GOLD, f"cg_{name}.npz"))
+    rp, cl, vl = oracle.read_mtx(os.path.join(GOLD, name + ".mtx"))
+    b = np.arange(1, len(rp), dtype=np.float64)
+    for tag, tol in (("1e-8", 1e-8), ("1e-24", 1e-24)):
+        x, res = oracle.cg_solve(rp, cl, vl, b, tol)
+        assert res.iterations == int(g[f"iters_{tag}"])
+        np.testing.assert_array_equal(x, g[f"x_{tag}"])
+
+
+def test_poisson_emitter_roundtrip(oracle, tmp_path):
+    for dim, nx, ny, nz in [(2, 5, 7, 1), (3, 3, 4, 5)]:
+        rp, cl, vl = oracle.poisson(dim, nx, ny, nz)
+        assert len(vl) == (2 * dim + 1) * (len(rp) - 1) - 2 * (
+            (ny * nz + nx * nz + nx * ny) if dim == 3 else (ny + nx))
+        p = str(tmp_path / "m.mtx")
+        oracle.write_mtx_lower(p, rp, cl, vl)
+        back = oracle.read_mtx(p)
+        for a, r in zip(back, (rp, cl, vl)):
+            np.testing.assert_array_equal(a, r)
+
+
+def test_cpu_baseline_matches_solver(oracle):
+    """The OpenMP baseline runs the same iteration (different reduction order)."""
+    rp, cl, vl = oracle.poisson(2, 32, 32, 1)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    t, x = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 30, 4)
+    xr, res = oracle.cg_solve(rp, cl, vl, b, 0.0, max_iter=30)
+    assert res.iterations == 30 and t > 0
+    assert rel(x, xr) < 1e-10

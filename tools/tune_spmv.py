@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""A/B the SpMV(+p.Ap) kernel variants on one device, interleaved rounds in
+one process (cdna_hip_programming.md §5.4 rule 24). Prints one JSON line per
+(config, variant): median/min us and algorithmic GB/s; checks every variant's
+y against variant 0 bit for bit.
+
+    python tools/tune_spmv.py [--configs 3d256,2d4096,irr] [--rounds 5] [--iters 20]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import conjugategradient_amd as cga  # noqa: E402
+from conjugategradient_amd._native import check, lib  # noqa: E402
+
+
+def matrix(q, name):
+    if name == "3d256":
+        return cga.Matrix.poisson(q, 3, 256, 256, 256)
+    if name == "3d128":
+        return cga.Matrix.poisson(q, 3, 128, 128, 128)
+    if name == "2d4096":
+        return cga.Matrix.poisson(q, 2, 4096, 4096, 1)
+    if name == "irr":
+        from tests.util import irregular_spd
+        rp, cl, vl = irregular_spd(1_585_478, mean_deg=3.83, seed=12345)
+        return cga.Matrix(q, vl, cl, rp)
+    raise ValueError(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="3d256,2d4096,irr")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    L = lib()
+    q = cga.Queue(0)
+    variants = [int(v) for v in a.variants.split(",")]
+    for name in a.configs.split(","):
+        A = matrix(q, name)
+        n, nnz = A.N(), A.NNZ()
+        x = cga.Vector(q, np.random.default_rng(0).standard_normal(n))
+        ys = {v: cga.Vector(q, n) for v in variants}
+        times = {v: [] for v in variants}
+        for _ in range(a.rounds):
+            for v in variants:
+                ms = C.c_double(0)
+                check(L.cgx_tune_spmv(q.handle, A.schedule(), v, x.ptr(), ys[v].ptr(), a.iters,
+                                      C.byref(ms)))
+                times[v].append(ms.value)
+        y0 = ys[variants[0]].to_numpy()
+        nbytes = 12 * nnz + 4 * (n + 1) + 16 * n
+        for v in variants:
+            t = np.array(times[v]) * 1e3
+            same = bool(np.array_equal(ys[v].to_numpy(), y0))
+            print(json.dumps({"config": name, "variant": v, "n": n, "nnz": nnz,
+                              "median_us": round(float(np.median(t)), 2),
+                              "min_us": round(float(t.min()), 2),
+                              "GBps_median": round(nbytes / (np.median(t) * 1e-6) / 1e9, 1),
+                              "bitexact_vs_v0": same}), flush=True)
+        del A, x, ys
+
+
+if __name__ == "__main__":
+    main()
