@@ -1,0 +1,88 @@
+"""The C++ drop-in boundary: include/CG.hpp & co. compile with the reference's
+own driver (test/Tester.cpp, unmodified) and with our example, and run on the
+GPU through libcgx.
+
+CPU tests compile (g++ and clang++) and check that without a device the
+program fails loudly. GPU tests run the binaries built by
+`make -C examples [dropin]` and compare against the oracle's golden outputs.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+LIBD = os.path.join(ROOT, "conjugategradient_amd")
+REF_TEST = "/root/reference/test"
+GOLD = os.path.join(ROOT, "tests", "golden")
+TESTER = os.path.join(ROOT, "build", "dropin", "tester")
+EXAMPLE = os.path.join(ROOT, "build", "examples", "solve_poisson")
+
+
+def _compile(cxx, srcs, out, extra=()):
+    cmd = [cxx, "-std=c++17", "-O1", "-I" + INC, *extra, *srcs, "-o", out, "-L" + LIBD, "-lcgx",
+           "-Wl,-rpath," + LIBD]
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+@pytest.mark.parametrize("cxx", ["g++", "/opt/rocm/lib/llvm/bin/clang++"])
+def test_reference_tester_compiles_unmodified(cxx, tmp_path):
+    if not os.path.isdir(REF_TEST):
+        pytest.skip("reference sources not present (GPU box)")
+    if not shutil.which(cxx) and not os.path.exists(cxx):
+        pytest.skip(f"{cxx} missing")
+    out = str(tmp_path / "tester")
+    r = _compile(cxx, [os.path.join(REF_TEST, "Tester.cpp"), os.path.join(REF_TEST, "mm_reader.cpp")],
+                 out, ["-I" + REF_TEST])
+    assert r.returncode == 0, r.stderr
+    # no GPU here: the program must fail loudly, not fall back
+    if not os.path.exists("/dev/kfd"):
+        p = subprocess.run([out, os.path.join(GOLD, "poisson2d_16.mtx")], capture_output=True,
+                           text=True)
+        assert p.returncode != 0 and "cgx_create" in p.stderr
+
+
+def test_example_compiles(tmp_path):
+    out = str(tmp_path / "solve_poisson")
+    r = _compile("g++", [os.path.join(ROOT, "examples", "solve_poisson.cpp")], out,
+                 ["-Wall", "-Werror"])
+    assert r.returncode == 0, r.stderr
+
+
+def _parse(stdout):
+    line = [ln for ln in stdout.splitlines() if re.match(r"^\d+ \d+ ", ln)][-1].split()
+    return int(line[0]), int(line[1]), float(line[2]), float(line[3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["poisson2d_16", "poisson2d_128", "poisson3d_16"])
+def test_reference_tester_runs_on_gpu(name):
+    if not os.path.exists(TESTER):
+        pytest.skip("build/dropin/tester not built (needs the reference sources at build time)")
+    p = subprocess.run([TESTER, os.path.join(GOLD, name + ".mtx")], capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    n, nnz, ms, acc = _parse(p.stdout)
+    g = np.load(os.path.join(GOLD, f"loader_{name}.npz"))
+    assert n == len(g["rowptr"]) - 1 and nnz == len(g["val"])
+    # Tester.cpp solves to 1e-24; accuracy() = ||b-Ax||^2/||x||^2 (Q6)
+    gold = float(np.load(os.path.join(GOLD, f"cg_{name}.npz"))["accuracy_1e-24"])
+    assert acc < 1e-24 and acc < 100 * gold
+
+
+@pytest.mark.gpu
+def test_example_runs_on_gpu(oracle):
+    exe = EXAMPLE
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "examples")], check=True)
+    p = subprocess.run([exe, "3", "16", "1e-8"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    n, nnz, ms, acc = _parse(p.stdout)
+    assert n == 4096 and nnz == 27136
+    it = int(re.search(r"iterations=(\d+)", p.stdout).group(1))
+    assert abs(it - 76) <= 2  # 16^3 at 1e-8 -> 76 bodies
+    assert acc < 1e-20
