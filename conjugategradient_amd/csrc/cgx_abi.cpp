@@ -240,7 +240,7 @@ extern "C" int cgx_create(int device, cgx_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&ctx->ws, sizeof(RedWs<double>));
   if (e == hipSuccess) e = hipMemset(ctx->ws, 0, sizeof(RedWs<double>));
   if (e == hipSuccess) e = hipMalloc(&ctx->scratch, 64);
-  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_pinned, 512, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&ctx->h_pinned, 1024, hipHostMallocDefault);
   if (e != hipSuccess) {
     cgx_destroy(ctx);
     return hip_fail(e, "cgx_create");

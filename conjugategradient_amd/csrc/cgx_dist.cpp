@@ -1,17 +1,21 @@
 // cgx_dist.cpp — row-partitioned CG across the GPUs of one node (SURVEY.md
-// §8(e)): one process per GPU, one RCCL communicator, contiguous row blocks.
+// §8(e)): one process per GPU, contiguous row blocks.
 //
 // The reference is single-device; this file adds the
 // partition. Per iteration:
 //   * halo exchange of p: every rank packs the p entries its neighbours need
-//     (k_gather) and ncclSend/ncclRecv's them inside one group; received
-//     values land in p's ghost area [n_local, n_local + n_ghost), grouped by
-//     owner, so the SpMV reads local and ghost entries from one array;
-//   * ncclAllReduce of p.Ap and r.r (one scalar each, in place on the device
+//     (k_gather) and sends them; received values land in p's ghost area
+//     [n_local, n_local + n_ghost), grouped by owner, so the SpMV reads local
+//     and ghost entries from one array;
+//   * all-reduce of p.Ap and of r.r (one scalar each, in place on the device
 //     scalar ring; every rank then derives identical alpha / beta / stop).
-// Setup (cgx_csr_create_dist) builds the plan from the local rows' global
-// column indices with the host-only helpers cgx_plan_ghosts/cgx_plan_remap,
-// which the CPU test-suite drives directly over a gloo world.
+// Transport: RCCL over xGMI (cgx_dist_init: ncclSend/ncclRecv inside one
+// group, ncclAllReduce), or a host-staged transport whose collectives are
+// caller callbacks (cgx_dist_init_host) — the latter lets several ranks share
+// one GPU (RCCL refuses that) so the whole device path is testable on a
+// single-GPU box. Setup (cgx_csr_create_dist) builds the plan from the local
+// rows' global column indices with the host-only helpers cgx_plan_ghosts /
+// cgx_plan_remap, which the CPU test-suite also drives over a gloo world.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,13 +39,88 @@ static int nccl_fail(ncclResult_t r, const char *what) {
     if (r_ != ncclSuccess) return ::cgx::nccl_fail(r_, #expr);  \
   } while (0)
 
+#define CGX_CB(expr)                                                   \
+  do {                                                                 \
+    int r_ = (expr);                                                   \
+    if (r_ != 0) {                                                     \
+      ::cgx::set_error("host transport callback %s failed (%d)", #expr, r_); \
+      return CGX_ENCCL;                                                \
+    }                                                                  \
+  } while (0)
+
 static ncclDataType_t nccl_type(int dtype) { return dtype == CGX_F32 ? ncclFloat : ncclDouble; }
 
+static bool multi(const cgx_ctx *ctx) { return ctx->world > 1 && (ctx->comm || ctx->host); }
+
+// ---- setup collectives on HOST buffers ----------------------------------
+static int comm_allgather(cgx_ctx *ctx, const void *mine, size_t bytes, void *all) {
+  std::memcpy((char *)all + bytes * ctx->rank, mine, bytes);
+  if (!multi(ctx)) return CGX_OK;
+  if (ctx->host) {
+    CGX_CB(ctx->host->allgather(ctx->host->user, mine, bytes, all));
+    return CGX_OK;
+  }
+  hipStream_t s = ctx->stream;
+  void *d = nullptr;
+  CGX_HIP(hipMalloc(&d, bytes * ctx->world));
+  CGX_HIP(hipMemcpyAsync((char *)d + bytes * ctx->rank, mine, bytes, hipMemcpyHostToDevice, s));
+  CGX_NCCL(ncclAllGather((char *)d + bytes * ctx->rank, d, bytes, ncclChar, ctx->comm, s));
+  CGX_HIP(hipMemcpyAsync(all, d, bytes * ctx->world, hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  CGX_HIP(hipFree(d));
+  return CGX_OK;
+}
+
+// pairwise exchange of host byte buffers with the listed peers
+static int comm_exchange(cgx_ctx *ctx, const std::vector<int> &peers,
+                         const std::vector<const void *> &send, const std::vector<size_t> &sbytes,
+                         const std::vector<void *> &recv, const std::vector<size_t> &rbytes) {
+  if (peers.empty()) return CGX_OK;
+  if (ctx->host) {
+    CGX_CB(ctx->host->exchange(ctx->host->user, (int)peers.size(), peers.data(), send.data(),
+                               sbytes.data(), recv.data(), rbytes.data()));
+    return CGX_OK;
+  }
+  hipStream_t s = ctx->stream;
+  size_t st = 0, rt = 0;
+  for (size_t i = 0; i < peers.size(); ++i) {
+    st += sbytes[i];
+    rt += rbytes[i];
+  }
+  char *ds = nullptr, *dr = nullptr;
+  CGX_HIP(hipMalloc(&ds, st + 1));
+  CGX_HIP(hipMalloc(&dr, rt + 1));
+  size_t so = 0, ro = 0;
+  for (size_t i = 0; i < peers.size(); ++i) {
+    if (sbytes[i]) CGX_HIP(hipMemcpyAsync(ds + so, send[i], sbytes[i], hipMemcpyHostToDevice, s));
+    so += sbytes[i];
+  }
+  CGX_NCCL(ncclGroupStart());
+  so = ro = 0;
+  for (size_t i = 0; i < peers.size(); ++i) {
+    if (sbytes[i]) CGX_NCCL(ncclSend(ds + so, sbytes[i], ncclChar, peers[i], ctx->comm, s));
+    if (rbytes[i]) CGX_NCCL(ncclRecv(dr + ro, rbytes[i], ncclChar, peers[i], ctx->comm, s));
+    so += sbytes[i];
+    ro += rbytes[i];
+  }
+  CGX_NCCL(ncclGroupEnd());
+  ro = 0;
+  for (size_t i = 0; i < peers.size(); ++i) {
+    if (rbytes[i]) CGX_HIP(hipMemcpyAsync(recv[i], dr + ro, rbytes[i], hipMemcpyDeviceToHost, s));
+    ro += rbytes[i];
+  }
+  CGX_HIP(hipStreamSynchronize(s));
+  CGX_HIP(hipFree(ds));
+  CGX_HIP(hipFree(dr));
+  return CGX_OK;
+}
+
+// ---- per-iteration collectives on DEVICE buffers ------------------------
 int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
   if (!A->dist) return CGX_OK;
   cgx_ctx *ctx = A->ctx;
   Halo &h = A->halo;
-  if (ctx->world == 1 || (h.n_ghost == 0 && h.send_total == 0)) return CGX_OK;
+  if (!multi(ctx) || (h.n_ghost == 0 && h.send_total == 0)) return CGX_OK;
   const size_t es = dtype_size(A->dtype);
   if (h.send_total > 0) {
     if (A->dtype == CGX_F32)
@@ -50,6 +129,29 @@ int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
     else
       CGX_HIP(Launch<double>::gather((const double *)vec_ext, h.d_send_idx, h.send_total,
                                      (double *)h.d_send_buf, s));
+  }
+  if (ctx->host) {
+    // stage through pinned host memory, exchange by callback, copy back
+    char *hs = (char *)h.h_send, *hr = (char *)h.h_recv;
+    if (h.send_total)
+      CGX_HIP(hipMemcpyAsync(hs, h.d_send_buf, (size_t)h.send_total * es, hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    std::vector<const void *> sp;
+    std::vector<void *> rp;
+    std::vector<size_t> sb, rb;
+    for (size_t i = 0; i < h.nbr.size(); ++i) {
+      sp.push_back(hs + (size_t)h.send_off[i] * es);
+      sb.push_back((size_t)h.send_cnt[i] * es);
+      rp.push_back(hr + (size_t)h.recv_off[i] * es);
+      rb.push_back((size_t)h.recv_cnt[i] * es);
+    }
+    CGX_CB(ctx->host->exchange(ctx->host->user, (int)h.nbr.size(), h.nbr.data(), sp.data(),
+                               sb.data(), rp.data(), rb.data()));
+    if (h.n_ghost)
+      CGX_HIP(hipMemcpyAsync((char *)vec_ext + (size_t)A->dev.n * es, hr, (size_t)h.n_ghost * es,
+                             hipMemcpyHostToDevice, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    return CGX_OK;
   }
   const ncclDataType_t t = nccl_type(A->dtype);
   CGX_NCCL(ncclGroupStart());
@@ -66,7 +168,25 @@ int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
 }
 
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s) {
-  if (!ctx->comm || ctx->world == 1) return CGX_OK;
+  if (!multi(ctx)) return CGX_OK;
+  if (ctx->host) {
+    CGX_REQUIRE(count <= 8, CGX_EINVAL, "host all-reduce of %d values", count);
+    const size_t es = dtype_size(dtype);
+    auto *h = (char *)ctx->h_pinned + 512;  // [0, 512) is cgx_cg_run's poll staging
+    CGX_HIP(hipMemcpyAsync(h, d_val, es * count, hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    double v[8];
+    for (int i = 0; i < count; ++i)
+      v[i] = dtype == CGX_F32 ? (double)((float *)h)[i] : ((double *)h)[i];
+    CGX_CB(ctx->host->allreduce(ctx->host->user, v, count));
+    for (int i = 0; i < count; ++i) {
+      if (dtype == CGX_F32) ((float *)h)[i] = (float)v[i];
+      else ((double *)h)[i] = v[i];
+    }
+    CGX_HIP(hipMemcpyAsync(d_val, h, es * count, hipMemcpyHostToDevice, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    return CGX_OK;
+  }
   CGX_NCCL(ncclAllReduce(d_val, d_val, (size_t)count, nccl_type(dtype), ncclSum, ctx->comm, s));
   return CGX_OK;
 }
@@ -74,14 +194,19 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
 int dist_destroy_halo(cgx_csr *A) {
   if (A->halo.d_send_idx) (void)hipFree(A->halo.d_send_idx);
   if (A->halo.d_send_buf) (void)hipFree(A->halo.d_send_buf);
+  if (A->halo.h_send) (void)hipHostFree(A->halo.h_send);
+  if (A->halo.h_recv) (void)hipHostFree(A->halo.h_recv);
   A->halo.d_send_idx = nullptr;
   A->halo.d_send_buf = nullptr;
+  A->halo.h_send = A->halo.h_recv = nullptr;
   return CGX_OK;
 }
 
 int dist_comm_destroy(cgx_ctx *ctx) {
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   ctx->comm = nullptr;
+  delete ctx->host;
+  ctx->host = nullptr;
   return CGX_OK;
 }
 
@@ -102,6 +227,11 @@ extern "C" int cgx_plan_ghosts(int64_t n_local, int64_t row_begin, int64_t nnz, 
   CGX_REQUIRE(col || nnz == 0, CGX_EINVAL, "col is NULL");
   CGX_REQUIRE(n_ghost && ghosts && recv_cnt && begins && counts && world >= 1, CGX_EINVAL,
               "NULL argument");
+  // ghosts sorted by global index are grouped by owner only when the row
+  // ranges are ordered by rank
+  for (int r = 1; r < world; ++r)
+    CGX_REQUIRE(begins[r] >= begins[r - 1] + counts[r - 1], CGX_EINVAL,
+                "row ranges must be contiguous and ordered by rank");
   const int64_t lo = row_begin, hi = row_begin + n_local;
   std::vector<int64_t> g;
   for (int64_t k = 0; k < nnz; ++k) {
@@ -111,18 +241,13 @@ extern "C" int cgx_plan_ghosts(int64_t n_local, int64_t row_begin, int64_t nnz, 
   std::sort(g.begin(), g.end());
   g.erase(std::unique(g.begin(), g.end()), g.end());
   std::fill(recv_cnt, recv_cnt + world, 0);
-  for (int64_t c : g) {
-    int owner = -1;
-    for (int r = 0; r < world; ++r)
-      if (c >= begins[r] && c < begins[r] + counts[r]) { owner = r; break; }
-    CGX_REQUIRE(owner >= 0, CGX_EINVAL, "column %lld is owned by no rank", (long long)c);
+  int owner = 0;
+  for (int64_t c : g) {  // g ascending and ranges ordered: owner only grows
+    while (owner < world && c >= begins[owner] + counts[owner]) ++owner;
+    CGX_REQUIRE(owner < world && c >= begins[owner], CGX_EINVAL,
+                "column %lld is owned by no rank", (long long)c);
     recv_cnt[owner] += 1;
   }
-  // ghosts sorted by global index are grouped by owner only when the row
-  // ranges are ordered by rank; cgx_csr_create_dist requires that.
-  for (int r = 1; r < world; ++r)
-    CGX_REQUIRE(begins[r] >= begins[r - 1] + counts[r - 1], CGX_EINVAL,
-                "row ranges must be contiguous and ordered by rank");
   *n_ghost = (int64_t)g.size();
   *ghosts = (int64_t *)std::malloc(std::max<size_t>(g.size(), 1) * sizeof(int64_t));
   std::copy(g.begin(), g.end(), *ghosts);
@@ -162,7 +287,7 @@ extern "C" int cgx_row_blocks(const int *rowptr, int64_t n, int64_t *nrb, int **
 }
 
 // ===========================================================================
-// RCCL communicator
+// communicators
 // ===========================================================================
 extern "C" int cgx_nccl_unique_id(char *id_out, size_t len) {
   CGX_REQUIRE(id_out && len >= sizeof(ncclUniqueId), CGX_EINVAL, "buffer too small (%zu < %zu)",
@@ -176,13 +301,24 @@ extern "C" int cgx_nccl_unique_id(char *id_out, size_t len) {
 extern "C" int cgx_dist_init(cgx_ctx *ctx, int rank, int world, const char *id, size_t len) {
   CGX_REQUIRE(ctx && id && len >= sizeof(ncclUniqueId), CGX_EINVAL, "bad argument");
   CGX_REQUIRE(world >= 1 && rank >= 0 && rank < world, CGX_EINVAL, "bad rank/world");
-  CGX_REQUIRE(!ctx->comm, CGX_ESTATE, "communicator already initialised");
+  CGX_REQUIRE(!ctx->comm && !ctx->host, CGX_ESTATE, "communicator already initialised");
   CGX_HIP(hipSetDevice(ctx->device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclComm_t comm = nullptr;
   CGX_NCCL(ncclCommInitRank(&comm, world, uid, rank));
   ctx->comm = comm;
+  ctx->rank = rank;
+  ctx->world = world;
+  return CGX_OK;
+}
+
+extern "C" int cgx_dist_init_host(cgx_ctx *ctx, int rank, int world, cgx_allgather_fn ag,
+                                  cgx_allreduce_fn ar, cgx_exchange_fn ex, void *user) {
+  CGX_REQUIRE(ctx && ag && ar && ex, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(world >= 1 && rank >= 0 && rank < world, CGX_EINVAL, "bad rank/world");
+  CGX_REQUIRE(!ctx->comm && !ctx->host, CGX_ESTATE, "communicator already initialised");
+  ctx->host = new HostComm{ag, ar, ex, user};
   ctx->rank = rank;
   ctx->world = world;
   return CGX_OK;
@@ -197,11 +333,11 @@ extern "C" int cgx_dist_rank(cgx_ctx *ctx, int *rank, int *world) {
 
 extern "C" int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value) {
   CGX_REQUIRE(ctx && value, CGX_EINVAL, "NULL argument");
-  if (!ctx->comm || ctx->world == 1) return CGX_OK;
+  if (!multi(ctx)) return CGX_OK;
   CGX_HIP(hipSetDevice(ctx->device));
   CGX_HIP(hipMemcpyAsync(ctx->scratch, value, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  CGX_NCCL(ncclAllReduce(ctx->scratch, ctx->scratch, 1, ncclDouble, ncclSum, ctx->comm,
-                         ctx->stream));
+  int rc = dist_allreduce_scalar(ctx, ctx->scratch, CGX_F64, 1, ctx->stream);
+  if (rc) return rc;
   CGX_HIP(hipMemcpyAsync(value, ctx->scratch, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CGX_HIP(hipStreamSynchronize(ctx->stream));
   return CGX_OK;
@@ -214,56 +350,42 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
                                    int64_t n_local, int64_t nnz_local, const int *d_rowptr,
                                    int *d_col, const void *d_val, int dtype, cgx_csr **out) {
   CGX_REQUIRE(ctx && out && d_rowptr && d_col && d_val, CGX_EINVAL, "NULL argument");
-  CGX_REQUIRE(ctx->comm || ctx->world == 1, CGX_ESTATE, "cgx_dist_init first");
+  CGX_REQUIRE(ctx->world == 1 || multi(ctx), CGX_ESTATE, "cgx_dist_init first");
   CGX_REQUIRE(n_local >= 1 && row_begin >= 0 && row_begin + n_local <= n_global, CGX_EINVAL,
               "bad local row range");
+  CGX_REQUIRE(dtype == CGX_F64 || dtype == CGX_F32, CGX_EINVAL, "bad dtype %d", dtype);
   CGX_HIP(hipSetDevice(ctx->device));
+  *out = nullptr;
   hipStream_t s = ctx->stream;
   const int world = ctx->world, me = ctx->rank;
+  int rc;
   // 1. every rank's row range
   std::vector<int64_t> part(2 * (size_t)world, 0);
-  {
-    int64_t mine[2] = {row_begin, n_local};
-    void *d = nullptr;
-    CGX_HIP(hipMalloc(&d, part.size() * sizeof(int64_t)));
-    CGX_HIP(hipMemcpyAsync((int64_t *)d + 2 * me, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-    if (world > 1)
-      CGX_NCCL(ncclAllGather((int64_t *)d + 2 * me, d, 2, ncclInt64, ctx->comm, s));
-    CGX_HIP(hipMemcpyAsync(part.data(), d, part.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    CGX_HIP(hipStreamSynchronize(s));
-    (void)hipFree(d);
-  }
+  const int64_t mine[2] = {row_begin, n_local};
+  if ((rc = comm_allgather(ctx, mine, sizeof(mine), part.data()))) return rc;
   std::vector<int64_t> begins(world), counts(world);
   for (int r = 0; r < world; ++r) {
     begins[r] = part[2 * r];
     counts[r] = part[2 * r + 1];
   }
-  // 2. local structure to the host
+  // 2. local structure to the host, ghost list
   std::vector<int> hrp((size_t)n_local + 1), hcol((size_t)nnz_local);
   CGX_HIP(hipMemcpyAsync(hrp.data(), d_rowptr, hrp.size() * sizeof(int), hipMemcpyDeviceToHost, s));
   CGX_HIP(hipMemcpyAsync(hcol.data(), d_col, hcol.size() * sizeof(int), hipMemcpyDeviceToHost, s));
   CGX_HIP(hipStreamSynchronize(s));
+  CGX_REQUIRE(hrp[0] == 0 && hrp[n_local] == nnz_local, CGX_EINVAL,
+              "local rowptr must run from 0 to nnz_local");
   int64_t n_ghost = 0;
-  int64_t *ghosts = nullptr;
+  int64_t *gp = nullptr;
   std::vector<int64_t> recv_cnt(world, 0);
-  int rc = cgx_plan_ghosts(n_local, row_begin, nnz_local, hcol.data(), world, begins.data(),
-                           counts.data(), &n_ghost, &ghosts, recv_cnt.data());
-  if (rc) return rc;
-  // 3. all-to-all of counts via an all-gather of the world x world matrix
+  if ((rc = cgx_plan_ghosts(n_local, row_begin, nnz_local, hcol.data(), world, begins.data(),
+                            counts.data(), &n_ghost, &gp, recv_cnt.data())))
+    return rc;
+  std::vector<int64_t> ghosts(gp, gp + n_ghost);
+  cgx_free_host(gp);
+  // 3. every rank's receive counts -> my send counts
   std::vector<int64_t> cmat((size_t)world * world, 0);
-  {
-    void *d = nullptr;
-    CGX_HIP(hipMalloc(&d, cmat.size() * sizeof(int64_t)));
-    CGX_HIP(hipMemcpyAsync((int64_t *)d + (size_t)world * me, recv_cnt.data(),
-                           world * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    if (world > 1)
-      CGX_NCCL(ncclAllGather((int64_t *)d + (size_t)world * me, d, (size_t)world, ncclInt64,
-                             ctx->comm, s));
-    CGX_HIP(hipMemcpyAsync(cmat.data(), d, cmat.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    CGX_HIP(hipStreamSynchronize(s));
-    (void)hipFree(d);
-  }
-  // 4. request lists: I send the global ids I need to each owner
+  if ((rc = comm_allgather(ctx, recv_cnt.data(), world * sizeof(int64_t), cmat.data()))) return rc;
   auto *A = new cgx_csr();
   A->ctx = ctx;
   A->dtype = dtype;
@@ -285,75 +407,68 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     soff += sc_;
   }
   h.send_total = soff;
+  // 4. request lists: the global ids I need go to their owners
+  std::vector<int> req(ghosts.begin(), ghosts.end()), inc((size_t)std::max<int64_t>(soff, 1));
   {
-    std::vector<int> greq((size_t)std::max<int64_t>(n_ghost, 1));
-    for (int64_t i = 0; i < n_ghost; ++i) greq[i] = (int)ghosts[i];
-    int *d_req = nullptr, *d_inc = nullptr;
-    hipError_t e = hipMalloc(&d_req, greq.size() * sizeof(int));
-    if (e == hipSuccess) e = hipMalloc(&d_inc, (size_t)std::max<int64_t>(soff, 1) * sizeof(int));
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_req, greq.data(), greq.size() * sizeof(int), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-      cgx_free_host(ghosts);
+    std::vector<const void *> sp;
+    std::vector<void *> rp;
+    std::vector<size_t> sb, rb;
+    for (size_t i = 0; i < h.nbr.size(); ++i) {
+      sp.push_back(req.data() + h.recv_off[i]);
+      sb.push_back((size_t)h.recv_cnt[i] * sizeof(int));
+      rp.push_back(inc.data() + h.send_off[i]);
+      rb.push_back((size_t)h.send_cnt[i] * sizeof(int));
+    }
+    if ((rc = comm_exchange(ctx, h.nbr, sp, sb, rp, rb))) {
       cgx_csr_destroy(A);
-      return hip_fail(e, "cgx_csr_create_dist(requests)");
-    }
-    if (!h.nbr.empty()) {
-      CGX_NCCL(ncclGroupStart());
-      for (size_t i = 0; i < h.nbr.size(); ++i) {
-        if (h.recv_cnt[i] > 0)
-          CGX_NCCL(ncclSend(d_req + h.recv_off[i], (size_t)h.recv_cnt[i], ncclInt32, h.nbr[i],
-                            ctx->comm, s));
-        if (h.send_cnt[i] > 0)
-          CGX_NCCL(ncclRecv(d_inc + h.send_off[i], (size_t)h.send_cnt[i], ncclInt32, h.nbr[i],
-                            ctx->comm, s));
-      }
-      CGX_NCCL(ncclGroupEnd());
-    }
-    std::vector<int> inc((size_t)std::max<int64_t>(soff, 1));
-    CGX_HIP(hipMemcpyAsync(inc.data(), d_inc, inc.size() * sizeof(int), hipMemcpyDeviceToHost, s));
-    CGX_HIP(hipStreamSynchronize(s));
-    (void)hipFree(d_req);
-    (void)hipFree(d_inc);
-    for (int64_t i = 0; i < soff; ++i) {
-      const int64_t g = inc[i];
-      if (g < row_begin || g >= row_begin + n_local) {
-        cgx_free_host(ghosts);
-        cgx_csr_destroy(A);
-        set_error("rank %d was asked for row %lld it does not own", me, (long long)g);
-        return CGX_EINVAL;
-      }
-      inc[i] = (int)(g - row_begin);
-    }
-    const size_t es = dtype_size(dtype);
-    e = hipMalloc(&h.d_send_idx, (size_t)std::max<int64_t>(soff, 1) * sizeof(int));
-    if (e == hipSuccess) e = hipMalloc(&h.d_send_buf, (size_t)std::max<int64_t>(soff, 1) * es);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(h.d_send_idx, inc.data(), (size_t)soff * sizeof(int),
-                         hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-      cgx_free_host(ghosts);
-      cgx_csr_destroy(A);
-      return hip_fail(e, "cgx_csr_create_dist(send plan)");
+      return rc;
     }
   }
+  for (int64_t i = 0; i < soff; ++i) {
+    const int64_t g = inc[i];
+    if (g < row_begin || g >= row_begin + n_local) {
+      cgx_csr_destroy(A);
+      set_error("rank %d was asked for row %lld it does not own", me, (long long)g);
+      return CGX_EINVAL;
+    }
+    inc[i] = (int)(g - row_begin);
+  }
+  const size_t es = dtype_size(dtype);
+  hipError_t e = hipMalloc(&h.d_send_idx, (size_t)std::max<int64_t>(soff, 1) * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&h.d_send_buf, (size_t)std::max<int64_t>(soff, 1) * es);
+  if (e == hipSuccess && soff)
+    e = hipMemcpyAsync(h.d_send_idx, inc.data(), (size_t)soff * sizeof(int),
+                       hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && ctx->host) {
+    e = hipHostMalloc(&h.h_send, (size_t)std::max<int64_t>(soff, 1) * es, hipHostMallocDefault);
+    if (e == hipSuccess)
+      e = hipHostMalloc(&h.h_recv, (size_t)std::max<int64_t>(n_ghost, 1) * es,
+                        hipHostMallocDefault);
+  }
+  if (e != hipSuccess) {
+    cgx_csr_destroy(A);
+    return hip_fail(e, "cgx_csr_create_dist(send plan)");
+  }
   // 5. columns to local numbering, back to the device
-  rc = cgx_plan_remap(n_local, row_begin, nnz_local, hcol.data(), n_ghost, ghosts);
-  cgx_free_host(ghosts);
-  if (rc) {
+  if ((rc = cgx_plan_remap(n_local, row_begin, nnz_local, hcol.data(), n_ghost, ghosts.data()))) {
     cgx_csr_destroy(A);
     return rc;
   }
-  CGX_HIP(hipMemcpyAsync(d_col, hcol.data(), hcol.size() * sizeof(int), hipMemcpyHostToDevice, s));
-  // 6. SpMV schedule over the local rows
+  e = hipMemcpyAsync(d_col, hcol.data(), hcol.size() * sizeof(int), hipMemcpyHostToDevice, s);
+  // 6. SpMV schedule over the local rows (+ entry offsets)
   int mx = 0;
   std::vector<int> rb = build_row_blocks(hrp.data(), n_local, &mx);
   const size_t nrb1 = rb.size();
   rb.resize(2 * nrb1);
   for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = hrp[rb[i]];
-  CGX_HIP(hipMalloc(&A->d_rb, rb.size() * sizeof(int)));
-  CGX_HIP(hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s));
-  CGX_HIP(hipStreamSynchronize(s));
+  if (e == hipSuccess) e = hipMalloc(&A->d_rb, rb.size() * sizeof(int));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    cgx_csr_destroy(A);
+    return hip_fail(e, "cgx_csr_create_dist(schedule)");
+  }
   A->max_row_nnz = mx;
   A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, A->d_rb + nrb1,
                   (int)nrb1 - 1};

@@ -45,7 +45,17 @@ struct Halo {
   std::vector<int64_t> send_off;   // offset inside send_idx / send_buf
   int *d_send_idx = nullptr;       // local row indices to pack, all nbrs
   void *d_send_buf = nullptr;      // packed values
+  void *h_send = nullptr;          // pinned staging (host transport only)
+  void *h_recv = nullptr;
   int64_t send_total = 0;
+};
+
+// Host-staged transport (cgx_dist_init_host): collectives are callbacks.
+struct HostComm {
+  cgx_allgather_fn allgather;
+  cgx_allreduce_fn allreduce;
+  cgx_exchange_fn exchange;
+  void *user;
 };
 
 }  // namespace cgx
@@ -55,9 +65,10 @@ struct cgx_ctx {
   hipStream_t stream = nullptr;
   void *ws = nullptr;           // cgx::RedWs<double> (large enough for float)
   void *scratch = nullptr;      // 2 doubles for accuracy() results
-  void *h_pinned = nullptr;     // pinned host staging (256 B)
+  void *h_pinned = nullptr;     // pinned host staging (1 KiB: polls | host all-reduce)
   // multi-GPU
   ncclComm *comm = nullptr;
+  cgx::HostComm *host = nullptr;
   int rank = 0, world = 1;
 };
 

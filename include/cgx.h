@@ -142,6 +142,20 @@ int cgx_iota(cgx_ctx *ctx, int dtype, void *d_b, int64_t n, double offset);
 int cgx_nccl_unique_id(char *id_out, size_t len);            /* len >= 128 */
 int cgx_dist_init(cgx_ctx *ctx, int rank, int world, const char *id, size_t len);
 int cgx_dist_rank(cgx_ctx *ctx, int *rank, int *world);
+/* Host-staged transport: the same partitioned solver with every collective
+ * done by caller callbacks on HOST buffers (return 0 on success). Used to run
+ * several ranks on one GPU (RCCL refuses that) in tests; slow by design.
+ *   allgather: recv[world * bytes] <- every rank's `bytes` from send
+ *   allreduce: vals[count] <- element-wise sum over ranks (in place)
+ *   exchange : for i < n, send[i] (send_bytes[i]) to peers[i] and receive
+ *              recv_bytes[i] from peers[i] into recv[i] */
+typedef int (*cgx_allgather_fn)(void *user, const void *send, size_t bytes, void *recv);
+typedef int (*cgx_allreduce_fn)(void *user, double *vals, int count);
+typedef int (*cgx_exchange_fn)(void *user, int n, const int *peers, const void *const *send,
+                               const size_t *send_bytes, void *const *recv,
+                               const size_t *recv_bytes);
+int cgx_dist_init_host(cgx_ctx *ctx, int rank, int world, cgx_allgather_fn allgather,
+                       cgx_allreduce_fn allreduce, cgx_exchange_fn exchange, void *user);
 /* Local block of a globally row-partitioned matrix: rows
  * [row_begin, row_begin + n_local) with GLOBAL column indices (device arrays,
  * caller-owned, d_col is rewritten in place to local/ghost numbering).

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Multi-rank check of libcgx's RCCL path (cgx_dist.cpp), one process per
+rank, launched with torch.distributed.run:
+
+  python -m torch.distributed.run --nproc-per-node W --master-addr 127.0.0.1 \
+      --master-port P tools/dist_check.py [--grid 32] [--tol 1e-8]
+
+Rank r drives device (LOCAL_RANK % visible devices), so W ranks can share
+one GPU when the communication library allows it. The global 3-D Poisson
+matrix is split in contiguous row blocks; every rank generates its own rows
+(global column indices) on the device, builds the halo plan
+(cgx_csr_create_dist) and solves with cgx_cg_solve. Rank 0 gathers x and
+compares with the oracle (single-process CPU restatement). Prints one JSON
+line with the verdict.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+import torch.distributed as dist  # noqa: E402
+
+import conjugategradient_amd as cga  # noqa: E402
+from conjugategradient_amd._native import F64, check, lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--tol", type=float, default=1e-8)
+    ap.add_argument("--transport", choices=["rccl", "host"], default="rccl")
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist.init_process_group("gloo")
+    L = lib()
+    dev = local % max(1, cga.device_count())
+    q = cga.Queue(dev)
+    if a.transport == "host":
+        from conjugategradient_amd.hostcomm import HostTransport
+        transport = HostTransport()
+        transport.attach(q)
+    else:
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            check(L.cgx_nccl_unique_id(uid, 128))
+        obj = [bytes(uid.raw) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        check(L.cgx_dist_init(q.handle, rank, world, obj[0], 128))
+    g = a.grid
+    n = g * g * g
+    base, extra = divmod(n, world)
+    counts = [base + (r < extra) for r in range(world)]
+    begin = sum(counts[:rank])
+    nl = counts[rank]
+    nnz = L.cgx_poisson_nnz(3, g, g, g, begin, begin + nl)
+    rows = cga.DeviceArray(q, nl + 1, np.int32)
+    cols = cga.DeviceArray(q, nnz, np.int32)
+    vals = cga.DeviceArray(q, nnz, np.float64)
+    check(L.cgx_poisson_fill(q.handle, F64, 3, g, g, g, begin, begin + nl, rows.ptr, cols.ptr,
+                             vals.ptr))
+    A = C.c_void_p()
+    check(L.cgx_csr_create_dist(q.handle, n, begin, nl, nnz, rows.ptr, cols.ptr, vals.ptr, F64,
+                                C.byref(A)))
+    ghosts, nbrs = C.c_int64(), C.c_int()
+    check(L.cgx_csr_halo_info(A, C.byref(ghosts), C.byref(nbrs)))
+    b = cga.DeviceArray(q, nl, np.float64)
+    x = cga.DeviceArray(q, nl, np.float64)
+    check(L.cgx_iota(q.handle, F64, b.ptr, nl, float(begin)))
+    x.fill(0.0)
+    cg = C.c_void_p()
+    check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+    bodies, rxr = C.c_int64(), C.c_double()
+    check(L.cgx_cg_solve(cg, b.ptr, x.ptr, a.tol, -1, C.byref(bodies), C.byref(rxr)))
+    acc = C.c_double()
+    check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
+    parts = [None] * world
+    dist.all_gather_object(parts, (x.download().tolist(), int(ghosts.value), int(nbrs.value)))
+    if rank == 0:
+        from oracle import oracle as O
+        xg = np.concatenate([np.array(p[0]) for p in parts])
+        rp, cl, vl = O.poisson(3, g, g, g)
+        xr, res = O.cg_solve(rp, cl, vl, np.arange(1, n + 1, dtype=np.float64), a.tol)
+        relerr = float(np.linalg.norm(xg - xr) / np.linalg.norm(xr))
+        ok = relerr <= 1e-10 and abs(bodies.value - res.iterations) <= 2
+        print(json.dumps({"world": world, "transport": a.transport, "grid": g, "bodies": bodies.value,
+                          "oracle_bodies": res.iterations, "rel_err": relerr,
+                          "accuracy": acc.value, "ghosts": [p[1] for p in parts],
+                          "neighbours": [p[2] for p in parts], "ok": ok}), flush=True)
+    L.cgx_cg_destroy(cg)
+    L.cgx_csr_destroy(A)
+    q.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
