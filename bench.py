@@ -16,10 +16,13 @@ value = algorithmic HBM bytes of one iteration over the whole job
 (B_alg = 12 nnz + 4 (N+1) + 80 N) x iterations/s, in GB/s.
 Inputs are generated directly in HBM before the timed region.
 
-rank 0 also prints the dominant kernel's roofline (k_spmv_dot, timed with HIP
-events on the solver stream inside the timed region) and, at N = 1, a CPU
-baseline: the oracle's OpenMP restatement of the reference's iteration
-(oracle/cg_oracle.c) timed on a bounded sample of the same workload.
+The timed region replays hipGraphs of the iteration (no per-kernel events:
+recording events between kernels costs ~10 us per kernel). Right after it,
+the same solver runs `--profile-steps` more iterations with HIP events around
+every kernel on the solver stream; rank 0 reports the dominant kernel's
+roofline (k_spmv_dot) from those. At N = 1 rank 0 also times a CPU baseline:
+the oracle's OpenMP restatement of the reference's iteration
+(oracle/cg_oracle.c) on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -48,10 +51,13 @@ def b_alg(n: int, nnz: int) -> int:
     return 12 * nnz + 4 * (n + 1) + 80 * n
 
 
-def spmv_dot_bytes(n: int, nnz: int) -> int:
-    """k_spmv_dot per launch: val 8 + col 4 per entry, rowptr 4 per row,
-    p read once 8 per row, Ap written 8 per row."""
-    return 12 * nnz + 4 * (n + 1) + 16 * n
+def spmv_dot_bytes(n: int, nnz: int, fused: bool) -> int:
+    """Algorithmic bytes of one launch of the dominant kernel.
+    k_spmv_dot (3-kernel mode): val 8 + col 4 per entry, rowptr 4 per row,
+    p read 8 and Ap written 8 per row.
+    k_spmv_fused (fused mode): the same CSR stream, plus per row r, p_old, x
+    read (24) and p_new, x, Ap written (24)."""
+    return 12 * nnz + 4 * (n + 1) + (48 if fused else 16) * n
 
 
 def parse():
@@ -65,8 +71,15 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="time the steps without per-kernel HIP events")
+    ap.add_argument("--profile-steps", type=int, default=100,
+                    help="iterations timed per kernel with HIP events after the timed region "
+                         "(0: skip the roofline pass)")
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2], default=0,
+                    help="iteration structure (cgx_cg_set_mode): 0 auto (= 1), 1 three "
+                         "kernels, 2 fused (single GPU)")
+    ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
+                    help="N>1 collectives: RCCL (default) or the host-staged test transport "
+                         "(lets ranks share one GPU; rehearsal only, numbers meaningless)")
     return ap.parse_args()
 
 
@@ -100,9 +113,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     L = lib()
-    q = cga.Queue(local)
+    q = cga.Queue(dev)
     n3 = args.grid
     nz_global = n3 * world
     n_local = n3 * n3 * n3
@@ -110,7 +124,11 @@ def main():
     n_global = n_local * world
 
     # ---- RCCL communicator (N > 1) ---------------------------------------
-    if world > 1:
+    if world > 1 and args.transport == "host":
+        from conjugategradient_amd.hostcomm import HostTransport
+        transport = HostTransport()
+        transport.attach(q)
+    elif world > 1:
         uid = C.create_string_buffer(128)
         if rank == 0:
             check(L.cgx_nccl_unique_id(uid, 128))
@@ -137,16 +155,18 @@ def main():
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
                                None, C.byref(A)))
+    variant = C.c_int(0)
+    check(L.cgx_csr_variant(A, C.byref(variant)))
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
-    total = args.warmup + args.steps
+    check(L.cgx_cg_set_mode(cg, args.mode))
+    fused = args.mode == 2
+    total = args.warmup + args.steps + args.profile_steps
     check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total))
     bodies, stopped = C.c_int64(0), C.c_int(0)
     if args.warmup:
         check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
-    kt = not args.no_kernel_timing
-    check(L.cgx_cg_set_kernel_timing(cg, 1 if kt else 0))
 
     # ---- timed region --------------------------------------------------------
     if world > 1:
@@ -171,19 +191,25 @@ def main():
     its = args.steps / elapsed
     value = b_alg(n_global, nnz_global) * its / 1e9
 
+    # ---- per-kernel HIP-event pass (roofline) ---------------------------------
     avg = (C.c_double * 4)()
     calls = (C.c_int64 * 4)()
-    check(L.cgx_cg_kernel_times(cg, avg, calls))
     roof = None
-    if kt and calls[1] > 0:
-        kb = spmv_dot_bytes(n_local, nnz_local)
+    if args.profile_steps:
+        check(L.cgx_cg_set_kernel_timing(cg, 1))
+        check(L.cgx_cg_run(cg, args.profile_steps, C.byref(bodies), C.byref(stopped)))
+        check(L.cgx_cg_kernel_times(cg, avg, calls))
+        check(L.cgx_cg_set_kernel_timing(cg, 0))
+    if calls[1] > 0:
+        kb = spmv_dot_bytes(n_local, nnz_local, fused)
         ach = kb / (avg[1] * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_spmv_dot", "bytes_per_launch": kb,
-                "avg_us": round(avg[1] * 1e3, 2),
-                "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2),
-                                         "k_update_xp": round(avg[3] * 1e3, 2)}}
+                "kernel": "k_spmv_fused" if fused else "k_spmv_dot", "bytes_per_launch": kb,
+                "avg_us": round(avg[1] * 1e3, 2), "launches_timed": int(calls[1]),
+                "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2)}}
+        if not fused:
+            roof["other_kernels_avg_us"]["k_update_xp"] = round(avg[3] * 1e3, 2)
         pmc = os.path.join(ROOT, "profiles", "pmc_spmv_dot.json")
         if os.path.exists(pmc):
             try:
@@ -217,7 +243,9 @@ def main():
                                    f"{nz_global}), CSR fp64/int32, fused CG iteration",
                        "rows_global": n_global, "nnz_global": nnz_global,
                        "bytes_per_iteration": b_alg(n_global, nnz_global),
-                       "parallelism": f"rows{world}" if world > 1 else "single"},
+                       "parallelism": f"rows{world}" if world > 1 else "single",
+                       "iteration": "fused (2 kernels)" if fused else "3 kernels",
+                       "spmv_variant": int(variant.value)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

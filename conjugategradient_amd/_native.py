@@ -57,6 +57,8 @@ _SIGS = {
     "cgx_fill": (_i32, [_vp, _i32, _vp, _dbl, _sz]),
     "cgx_csr_create": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _i32, _vp, C.POINTER(_vp)]),
     "cgx_csr_destroy": (_i32, [_vp]),
+    "cgx_csr_set_tile": (_i32, [_vp, _i32]),
+    "cgx_csr_variant": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
                             C.POINTER(_i32)]),
     "cgx_spmv": (_i32, [_vp, _vp, _vp, _vp, _i64]),
@@ -74,6 +76,7 @@ _SIGS = {
     "cgx_cg_set_kernel_timing": (_i32, [_vp, _i32]),
     "cgx_cg_kernel_times": (_i32, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "cgx_cg_config": (_i32, [_vp, _i32, _i32]),
+    "cgx_cg_set_mode": (_i32, [_vp, _i32]),
     "cgx_accuracy": (_i32, [_vp, _vp, _vp, _vp, C.POINTER(_dbl)]),
     "cgx_poisson_nnz": (_i64, [_i32, _i32, _i32, _i32, _i64, _i64]),
     "cgx_poisson_fill": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _vp, _vp]),

@@ -357,6 +357,7 @@ class CG:
         self.final_rxr = float("nan")  # extension: rxr after the last body
         self.poll_every = 32
         self.use_graph = True
+        self.mode = 0  # cgx_cg_set_mode: 0 auto, 1 three kernels, 2 fused
 
     @classmethod
     def createCG(cls, dtype=np.float64, debug=Debuglevel.None_, device: int = 0) -> "CG":
@@ -416,6 +417,7 @@ class CG:
             self._cg = h
             self._cg_for = sched
             check(lib().cgx_cg_config(self._cg, self.poll_every, 1 if self.use_graph else 0))
+            check(lib().cgx_cg_set_mode(self._cg, self.mode))
         return self._cg
 
     def solve(self, improvement: float = 0.0, max_iter: int = -1) -> None:

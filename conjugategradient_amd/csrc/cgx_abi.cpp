@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -35,7 +36,9 @@ int hip_fail(hipError_t e, const char *what) {
   return CGX_EHIP;
 }
 
-std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz) {
+std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz, int tile) {
+  const int cap = tile - 6;                            // quad loads (kTileCap)
+  const int rows_max = tile / 8;  // 2048 -> 256, 1024 -> 128, 512 -> 64 rows
   std::vector<int> rb;
   rb.reserve((size_t)(n / 128 + 2));
   rb.push_back(0);
@@ -44,14 +47,14 @@ std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz
   while (row < n) {
     const int64_t start = row;
     int len = rowptr[row + 1] - rowptr[row];
-    if (len > kTileCap) {  // a long row gets a workgroup of its own
+    if (len > cap) {  // a long row gets a workgroup of its own
       mx = std::max(mx, len);
       ++row;
     } else {
       int64_t acc = 0;
-      while (row < n && row - start < kRowsPerBlock) {
+      while (row < n && row - start < rows_max) {
         len = rowptr[row + 1] - rowptr[row];
-        if (acc + len > kTileCap) break;
+        if (acc + len > cap) break;
         acc += len;
         mx = std::max(mx, len);
         ++row;
@@ -126,6 +129,7 @@ template <class F> int timed(cgx_cg *cg, int kid, hipStream_t s, F &&launch) {
 // iterations after the stop return at entry and would skew the averages.
 int harvest_events(cgx_cg *cg, int64_t active_iters) {
   int64_t iter_seen = 0;
+  const int last_kid = cg->fused ? 2 : 3;
   for (auto &pr : cg->ev_pending) {
     const int kid = pr.first;
     float ms = 0;
@@ -135,7 +139,7 @@ int harvest_events(cgx_cg *cg, int64_t active_iters) {
       cg->t_ms[kid] += ms;
       cg->t_calls[kid] += 1;
     }
-    if (kid == 3) ++iter_seen;
+    if (kid == last_kid) ++iter_seen;
   }
   cg->ev_pending.clear();
   cg->ev_used = 0;
@@ -163,8 +167,47 @@ template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   return CGX_OK;
 }
 
+// Fused iteration (single device): x/p update folded into the next SpMV.
+template <typename T> int enqueue_iter_fused(cgx_cg *cg, int slot) {
+  cgx_csr *A = cg->A;
+  hipStream_t s = cg->ctx->stream;
+  auto *st = (CgScalars<T> *)cg->st;
+  auto *ws = (RedWs<T> *)cg->ws;
+  T *P[2] = {(T *)cg->p, (T *)cg->p2};
+  T *pp = P[(slot + 3) & 1], *pc = P[slot & 1];
+  T *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
+  int rc;
+  if ((rc = timed(cg, 1, s, [&] {
+         return Launch<T>::spmv_fused(A->dev, r, pp, pc, x, Ap, st, slot, ws, s);
+       })))
+    return rc;
+  if ((rc = timed(cg, 2, s,
+                  [&] { return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, true); })))
+    return rc;
+  return CGX_OK;
+}
+
 int enqueue_iter_any(cgx_cg *cg, int slot) {
+  if (cg->fused)
+    return cg->dtype == CGX_F32 ? enqueue_iter_fused<float>(cg, slot)
+                                : enqueue_iter_fused<double>(cg, slot);
   return cg->dtype == CGX_F32 ? enqueue_iter<float>(cg, slot) : enqueue_iter<double>(cg, slot);
+}
+
+// Fused mode leaves the last body's x update pending: apply it (idempotent).
+int flush_pending_x(cgx_cg *cg) {
+  if (!cg->fused) return CGX_OK;
+  const int last = (cg->slot + 3) & 3;
+  hipStream_t s = cg->ctx->stream;
+  void *P[2] = {cg->p, cg->p2};
+  if (cg->dtype == CGX_F32)
+    CGX_HIP(Launch<float>::flush_x(cg->n, (float *)cg->x, (const float *)P[last & 1],
+                                   (CgScalars<float> *)cg->st, last, (RedWs<float> *)cg->ws, s));
+  else
+    CGX_HIP(Launch<double>::flush_x(cg->n, (double *)cg->x, (const double *)P[last & 1],
+                                    (CgScalars<double> *)cg->st, last, (RedWs<double> *)cg->ws,
+                                    s));
+  return CGX_OK;
 }
 
 void drop_graph(cgx_cg *cg) {
@@ -345,6 +388,8 @@ extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
   return CGX_OK;
 }
 
+int autotune_spmv(cgx_csr *A);
+
 // ===========================================================================
 // CSR
 // ===========================================================================
@@ -386,7 +431,7 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   A->ctx = ctx;
   A->dtype = dtype;
   A->max_row_nnz = mx;
-  A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, nullptr, (int)nrb1 - 1};
+  A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, nullptr, (int)nrb1 - 1, kTile};
   hipError_t e = hipMalloc(&A->d_rb, rb.size() * sizeof(int));
   if (e == hipSuccess)
     e = hipMemcpyAsync(A->d_rb, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -399,6 +444,11 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   A->dev.rb = A->d_rb;
   A->dev.rbk = A->d_rb + nrb1;
   A->n_global = n;
+  int rc = autotune_spmv(A);
+  if (rc) {
+    cgx_csr_destroy(A);
+    return rc;
+  }
   *out = A;
   return CGX_OK;
 }
@@ -414,12 +464,110 @@ extern "C" int cgx_csr_destroy(cgx_csr *A) {
   return CGX_OK;
 }
 
+// Rebuild the row-block schedule for another tile size (2048 or 1024).
+extern "C" int cgx_csr_set_tile(cgx_csr *A, int tile) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  CGX_REQUIRE(tile == 2048 || tile == 1024 || tile == 512, CGX_EINVAL,
+              "tile must be 2048, 1024 or 512 (wave tiles)");
+  if (tile == A->dev.tile) return CGX_OK;
+  DeviceGuard g(A->ctx->device);
+  hipStream_t s = A->ctx->stream;
+  const int64_t n = A->dev.n;
+  std::vector<int> hrp((size_t)n + 1);
+  CGX_HIP(hipMemcpyAsync(hrp.data(), A->dev.rowptr, hrp.size() * sizeof(int),
+                         hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  int mx = 0;
+  std::vector<int> rb = build_row_blocks(hrp.data(), n, &mx, tile);
+  const size_t nrb1 = rb.size();
+  rb.resize(2 * nrb1);
+  for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = hrp[rb[i]];
+  int *d = nullptr;
+  CGX_HIP(hipMalloc(&d, rb.size() * sizeof(int)));
+  CGX_HIP(hipMemcpyAsync(d, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  if (A->d_rb) CGX_HIP(hipFree(A->d_rb));
+  A->d_rb = d;
+  A->dev.rb = d;
+  A->dev.rbk = d + nrb1;
+  A->dev.nrb = (int)nrb1 - 1;
+  A->dev.tile = tile;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_variant(cgx_csr *A, int *variant) {
+  CGX_REQUIRE(A && variant, CGX_EINVAL, "NULL argument");
+  *variant = A->dev.variant;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, int *mx) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
   if (n) *n = A->dev.n;
   if (nnz) *nnz = A->dev.nnz;
   if (rbs) *rbs = A->dev.nrb;
   if (mx) *mx = A->max_row_nnz;
+  return CGX_OK;
+}
+
+// Pick the SpMV variant for this matrix on this device: the measured best
+// differs by matrix (non-temporal val/col loads help the 2-D 5-point matrix,
+// cost the 3-D 7-point one) and is cheap to measure — a few
+// launches on scratch vectors. $CGX_SPMV_VARIANT forces a variant.
+int autotune_spmv(cgx_csr *A) {
+  if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
+    A->dev.variant = std::atoi(env);
+    return CGX_OK;
+  }
+  const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
+  if (bytes < (int64_t(64) << 20)) return CGX_OK;  // small: the size heuristic
+  static const int cands[] = {13, 15};
+  cgx_ctx *ctx = A->ctx;
+  hipStream_t s = ctx->stream;
+  const size_t es = dtype_size(A->dtype);
+  const size_t nx = (size_t)(A->dev.n + A->halo.n_ghost);
+  void *x = nullptr, *y = nullptr, *st = nullptr;
+  hipError_t e = hipMalloc(&x, nx * es);
+  if (e == hipSuccess) e = hipMalloc(&y, nx * es);
+  if (e == hipSuccess) e = hipMalloc(&st, sizeof(CgScalars<double>));
+  if (e == hipSuccess) e = hipMemsetAsync(x, 0, nx * es, s);
+  if (e == hipSuccess) e = hipMemsetAsync(st, 0, sizeof(CgScalars<double>), s);
+  const int one = 1;
+  const size_t off = A->dtype == CGX_F32 ? offsetof(CgScalars<float>, active)
+                                         : offsetof(CgScalars<double>, active);
+  if (e == hipSuccess) e = hipMemcpyAsync((char *)st + off, &one, sizeof(int), hipMemcpyHostToDevice, s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  float best = 1e30f;
+  int best_v = 0;
+  for (int v : cands) {
+    float tot = 0;
+    for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
+      if (rep == 1) e = hipEventRecord(e0, s);
+      if (e != hipSuccess) break;
+      if (A->dtype == CGX_F32)
+        e = Launch<float>::spmv_dot_variant(v, A->dev, (const float *)x, (float *)y,
+                                            (CgScalars<float> *)st, (RedWs<float> *)ctx->ws, s);
+      else
+        e = Launch<double>::spmv_dot_variant(v, A->dev, (const double *)x, (double *)y,
+                                             (CgScalars<double> *)st, (RedWs<double> *)ctx->ws,
+                                             s);
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
+    if (e == hipSuccess && tot < best) {
+      best = tot;
+      best_v = v;
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  for (void *p : {x, y, st})
+    if (p) (void)hipFree(p);
+  CGX_HIP(e);
+  A->dev.variant = best_v;
   return CGX_OK;
 }
 
@@ -536,6 +684,7 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
   hipError_t e = hipMalloc(&cg->r, (size_t)cg->n * es);
   if (e == hipSuccess) e = hipMalloc(&cg->p, next * es);
   if (e == hipSuccess) e = hipMalloc(&cg->Ap, next * es);
+  if (e == hipSuccess && !A->dist) e = hipMalloc(&cg->p2, (size_t)cg->n * es);
   if (e == hipSuccess) e = hipMalloc(&cg->st, stb);
   if (e == hipSuccess) e = hipMalloc(&cg->ws, wsb);
   if (e == hipSuccess) e = hipMemsetAsync(cg->st, 0, stb, ctx->stream);
@@ -550,7 +699,23 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
     }
     return hip_fail(e, "cgx_cg_create");
   }
+  cg->fused = false;  // auto mode: three kernels (fused measured slower)
   *out = cg;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  CGX_REQUIRE(mode >= 0 && mode <= 2, CGX_EINVAL, "mode %d: 0 auto, 1 three kernels, 2 fused",
+              mode);
+  CGX_REQUIRE(!(mode == 2 && cg->A->dist), CGX_EUNSUPPORTED,
+              "the fused iteration runs on a single device (partitioned matrices use mode 1)");
+  const bool f = mode == 2;
+  if (f != cg->fused) {
+    CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
+    drop_graph(cg);
+  }
+  cg->fused = f;
   return CGX_OK;
 }
 
@@ -560,7 +725,7 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   (void)hipStreamSynchronize(cg->ctx->stream);
   drop_graph(cg);
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
-  for (void *p : {cg->r, cg->p, cg->Ap, cg->st, cg->ws})
+  for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws})
     if (p) (void)hipFree(p);
   delete cg;
   return CGX_OK;
@@ -590,6 +755,8 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
   if (max_bodies >= 0) cap = std::min<long long>(cap, std::max<long long>(max_bodies, 1));
   cg->b = b;
   cg->x = x;
+  if (cg->fused)  // p_{-1} = 0 for body 0 of the fused iteration
+    CGX_HIP(hipMemsetAsync(cg->p2, 0, (size_t)cg->n * dtype_size(cg->dtype), s));
   const void *xe = x;
   int rc;
   if (A->dist) {
@@ -690,6 +857,8 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
   if (rc) return rc;
+  if ((rc = flush_pending_x(cg))) return rc;
+  CGX_HIP(hipStreamSynchronize(s));
   if (cg->timing) {
     CGX_HIP(hipStreamSynchronize(s));
     const int64_t active_iters = last_bodies - (bodies_before < 0 ? 0 : bodies_before);

@@ -13,7 +13,7 @@ namespace cgx {
 // ---- launch geometry --------------------------------------------------------
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 constexpr int kTile = 2048;        // CSR entries staged in LDS per row block
-constexpr int kTileCap = kTile - 2; // entries a row block may hold (paired loads)
+constexpr int kTileCap = kTile - 6; // entries a row block may hold (quad loads overrun)
 constexpr int kRowsPerBlock = 256; // max rows per row block (one per thread)
 constexpr int kMaxGrid = 2048;     // persistent grid cap: 256 CUs x 8 WGs
 constexpr int kMaxRed = 2;         // values reduced together (accuracy: 2)
@@ -31,6 +31,7 @@ template <typename T> struct CgScalars {
   T tol;      // acc (CG.hpp:286)
   T pad_t;
   int active[4];
+  int xpend[4];      // fused iteration: body in slot s has its x update pending
   long long bodies;  // loop bodies executed (the reference's counter + 1)
   long long cap;     // max bodies: N+1 (CG.hpp:436) or a caller cap
   int stopped;       // 0 running, 1 stop rule (tol / NaN), 2 cap reached
@@ -53,6 +54,8 @@ struct CsrDev {
   const int *rb;   // row-block starts, nrb + 1 entries
   const int *rbk;  // rowptr[rb[i]], nrb + 1 entries
   int nrb;
+  int tile = kTile; // entries per row block the schedule was built for (2048 | 1024 | 512)
+  int variant = 0;  // SpMV variant picked for this matrix (0: size heuristic)
 };
 
 template <typename T> struct Launch {
@@ -67,7 +70,11 @@ template <typename T> struct Launch {
   static hipError_t spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                      CgScalars<T> *st, RedWs<T> *ws, hipStream_t s);
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                             RedWs<T> *ws, hipStream_t s);
+                             RedWs<T> *ws, hipStream_t s, bool fused = false);
+  static hipError_t spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
+                               CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s);
+  static hipError_t flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,
+                            RedWs<T> *ws, hipStream_t s);
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
                               int slot, hipStream_t s);
   static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,
@@ -90,7 +97,8 @@ template <typename T> struct Launch {
 enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 
 // host-side row-block schedule (cgx_abi.cpp)
-std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz);
+std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz,
+                                  int tile = kTile);
 
 __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, int64_t row);
 

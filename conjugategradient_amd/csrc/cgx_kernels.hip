@@ -29,6 +29,8 @@
 //    as in the reference's expressions.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cgx_internal.h"
 
 namespace cgx {
@@ -135,10 +137,21 @@ struct CsrArgs {
   const int *__restrict__ rb;   // first row of each row block (nrb + 1)
   const int *__restrict__ rbk;  // rowptr[rb[i]]: first entry of each row block
   int nrb;
+  int64_t n;
 };
 
-template <typename T> struct SpmvLds {
-  T prod[kTile + 2];  // + 2 scratch slots for branch-free out-of-range stores
+// Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
+// 128 rows per row block) — fewer registers per thread, more workgroups per
+// CU to hide the gather latency. The matrix's row-block schedule must have
+// been built for the same tile (cgx_csr_set_tile).
+template <int V> struct TileOf {
+  static constexpr int tile = (V & 64) ? 1024 : 2048;
+  static constexpr int cap = tile - 2;  // paired loads read up to 2 extra entries
+  static constexpr int rows = (V & 64) ? 128 : 256;
+};
+
+template <typename T, int TILE = kTile> struct SpmvLds {
+  T prod[TILE + 4];  // + 4 scratch slots for branch-free out-of-range stores
   int rp[kRowsPerBlock + 1];
   T red[4 * kMaxRed];
   int flag;
@@ -162,6 +175,20 @@ template <bool NT, typename P> __device__ __forceinline__ P ldg(const P *p) {
   else return *p;
 }
 
+// Where the SpMV takes its x_j from: a stored vector, or p_j computed on the
+// fly as r_j + beta * p_old_j (the fused iteration; the same expression the
+// reference evaluates for p, CG.hpp:418, so the value is bit-identical).
+template <typename T> struct GatherX {
+  const T *__restrict__ x;
+  __device__ __forceinline__ T operator()(int c) const { return x[c]; }
+};
+template <typename T> struct GatherP {
+  const T *__restrict__ r;
+  const T *__restrict__ pp;
+  T beta;
+  __device__ __forceinline__ T operator()(int c) const { return r[c] + beta * pp[c]; }
+};
+
 template <int V>
 __device__ __forceinline__ void work_range(int nrb, int &first, int &step, int &end) {
   const int G = gridDim.x;
@@ -177,10 +204,11 @@ __device__ __forceinline__ void work_range(int nrb, int &first, int &step, int &
   }
 }
 
-template <typename T, int V, class Epi>
+template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict__ val,
-                                          const T *__restrict__ x, Epi &epi,
-                                          SpmvLds<T> &sm) {
+                                          const Gather &x, Epi &epi,
+                                          SpmvLds<T, TileOf<V>::tile> &sm) {
+  using TL = TileOf<V>;
   constexpr bool NT = (V & 2) != 0;
   constexpr bool PAIRS = (V & 4) != 0;
   const int t = threadIdx.x;
@@ -193,11 +221,11 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
     __syncthreads();
     const int k0 = sm.rp[0];
     const int cnt = sm.rp[nrows] - k0;
-    if (cnt <= kTileCap) {
+    if (cnt <= TL::cap) {
       if (cnt > 0) {
         if constexpr (PAIRS) {
           using PV = typename PairOf<T>::V;
-          constexpr int U = kTile / (2 * kBlock);
+          constexpr int U = TL::tile / (2 * kBlock);
           const int ka = k0 & ~1;
           const int npairs = (k0 + cnt - ka + 1) >> 1;
           const PV *v2 = reinterpret_cast<const PV *>(val + ka);
@@ -213,8 +241,8 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
           T g0[U], g1[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            g0[u] = x[c[u].x];
-            g1[u] = x[c[u].y];
+            g0[u] = x(c[u].x);
+            g1[u] = x(c[u].y);
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -223,7 +251,7 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
             if (pos + 1 >= 0 && pos + 1 < cnt) sm.prod[pos + 1] = v[u].y * g1[u];
           }
         } else {
-          constexpr int U = kTile / kBlock;
+          constexpr int U = TL::tile / kBlock;
           T v[U];
           int c[U];
 #pragma unroll
@@ -234,7 +262,7 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
           }
           T g[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) g[u] = x[c[u]];
+          for (int u = 0; u < U; ++u) g[u] = x(c[u]);
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int k = t + u * kBlock;
@@ -254,7 +282,7 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
     } else {
       // One row longer than a tile (the schedule isolates such rows).
       T s[1] = {T(0)};
-      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x[A.col[k0 + k]];
+      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x(A.col[k0 + k]);
       block_sum<T, 1>(s, sm.red);
       if (t == 0) {
         epi.pre(r0);
@@ -270,13 +298,14 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
 // next are already in flight. Every load is issued unconditionally (clamped
 // to valid addresses) so the compiler's in-order vmcnt bookkeeping can wait
 // for the current block's gathers without draining the prefetch.
-template <typename T, int V, class Epi>
+template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__restrict__ val,
-                                               const T *__restrict__ x, Epi &epi,
-                                               SpmvLds<T> &sm) {
+                                               const Gather &x, Epi &epi,
+                                               SpmvLds<T, TileOf<V>::tile> &sm) {
+  using TL = TileOf<V>;
   constexpr bool NT = (V & 2) != 0;
   using PV = typename PairOf<T>::V;
-  constexpr int U = kTile / (2 * kBlock);
+  constexpr int U = TL::tile / (2 * kBlock);
   const int t = threadIdx.x;
   int b, step, end;
   work_range<V>(A.nrb, b, step, end);
@@ -310,28 +339,39 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
     T g0[U], g1[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      g0[u] = x[c[u].x];
-      g1[u] = x[c[u].y];
+      if constexpr ((V & 16) != 0) {  // ablation (timing only): no gathers
+        g0[u] = T(c[u].x & 1);
+        g1[u] = T(c[u].y & 1);
+      } else {
+        g0[u] = x(c[u].x);
+        g1[u] = x(c[u].y);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     PV vn[U];
     Int2 cn[U];
     issue(nk0, nk1, vn, cn);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((V & 32) != 0) {  // ablation (timing only): no LDS / row phase
+      T s = T(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += v[u].x * g0[u] + v[u].y * g1[u];
+      if (t < nrows) epi.row(r0 + t, s);
+    } else {
     {
       // branch-free: lanes outside [0, cnt) store into the scratch slots
       const int ka = k0 & ~1;
-      const int lim = min(cnt, kTileCap);
+      const int lim = min(cnt, TL::cap);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int pos = 2 * (t + u * kBlock) + ka - k0;
-        const int q0 = (pos >= 0 && pos < lim) ? pos : kTile;
-        const int q1 = (pos + 1 >= 0 && pos + 1 < lim) ? pos + 1 : kTile + 1;
+        const int q0 = (pos >= 0 && pos < lim) ? pos : TL::tile;
+        const int q1 = (pos + 1 >= 0 && pos + 1 < lim) ? pos + 1 : TL::tile + 1;
         sm.prod[q0] = v[u].x * g0[u];
         sm.prod[q1] = v[u].y * g1[u];
       }
     }
-    if (cnt <= kTileCap) {
+    if (cnt <= TL::cap) {
       __syncthreads();
       if (t < nrows) {
         T s = T(0);
@@ -343,7 +383,239 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
       // one row longer than a tile
       __syncthreads();
       T s[1] = {T(0)};
-      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x[A.col[k0 + k]];
+      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x(A.col[k0 + k]);
+      block_sum<T, 1>(s, sm.red);
+      if (t == 0) epi.row(r0, s[0]);
+      __syncthreads();
+    }
+    }
+    if (!has_next) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = vn[u];
+      c[u] = cn[u];
+    }
+    b = nb;
+    r0 = nr0;
+    r1 = nr1;
+    k0 = nk0;
+    k1 = nk1;
+  }
+}
+
+// Three-stage software pipeline (variant bit 128, paired loads): while the
+// current block b is multiplied, staged and summed, the gathers and values of
+// block b+1 and the column indices of block b+2 are in flight, so each
+// memory latency (HBM for val/col, L2 for the gathers) gets a whole block's
+// time to resolve instead of lying on the block's critical path. Loads are
+// issued unconditionally (clamped to valid addresses); the row epilogue's own
+// loads go out before the prefetches (vmcnt counts in issue order).
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_rows_deep(const CsrArgs &A, const T *__restrict__ val,
+                                               const Gather &x, Epi &epi,
+                                               SpmvLds<T, TileOf<V>::tile> &sm) {
+  using TL = TileOf<V>;
+  constexpr bool NT = (V & 2) != 0;
+  using PV = typename PairOf<T>::V;
+  constexpr int U = TL::tile / (2 * kBlock);
+  const int t = threadIdx.x;
+  int b, step, end;
+  work_range<V>(A.nrb, b, step, end);
+  if (b >= end) return;
+  // pair window [ka, ka + 2*np) of a block's entries [k0, k1)
+  auto window = [](int kk0, int kk1, int &ka, int &np) {
+    const bool ok = kk1 > kk0;  // empty blocks read pairs [0, 1] (nnz >= 2)
+    ka = ok ? (kk0 & ~1) : 0;
+    np = ok ? ((kk1 - ka + 1) >> 1) : 1;
+  };
+  auto load_c = [&](int kk0, int kk1, Int2(&cc)[U]) {
+    int ka, np;
+    window(kk0, kk1, ka, np);
+    const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
+#pragma unroll
+    for (int u = 0; u < U; ++u) cc[u] = ldg<NT>(c2 + min(t + u * kBlock, np - 1));
+  };
+  auto load_v = [&](int kk0, int kk1, PV(&vv)[U]) {
+    int ka, np;
+    window(kk0, kk1, ka, np);
+    const PV *v2 = reinterpret_cast<const PV *>(val + ka);
+#pragma unroll
+    for (int u = 0; u < U; ++u) vv[u] = ldg<NT>(v2 + min(t + u * kBlock, np - 1));
+  };
+  auto gather = [&](const Int2(&cc)[U], T(&g0)[U], T(&g1)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g0[u] = x(cc[u].x);
+      g1[u] = x(cc[u].y);
+    }
+  };
+  // blocks b (current), b1 = b + step, b2 = b + 2 step (clamped to the last)
+  int b1 = b + step < end ? b + step : b;
+  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  int k0n = A.rbk[b1], k1n = A.rbk[b1 + 1];
+  Int2 cN[U];
+  PV vC[U];
+  T gC0[U], gC1[U];
+  load_c(k0, k1, cN);
+  gather(cN, gC0, gC1);  // waits for block b's columns (prologue only)
+  load_v(k0, k1, vC);
+  load_c(k0n, k1n, cN);
+  for (;;) {
+    const int nb = b + step;
+    const bool has_next = nb < end;
+    const int b2 = b1 + step < end ? b1 + step : b1;
+    const int k0nn = A.rbk[b2], k1nn = A.rbk[b2 + 1];
+    const int nrows = r1 - r0, cnt = k1 - k0;
+    // this block's row operands (issued before the next stages' loads)
+    const int tr = min(t, max(nrows - 1, 0));
+    const int a = A.rowptr[r0 + tr] - k0, e = A.rowptr[r0 + tr + 1] - k0;
+    epi.pre(r0 + tr);
+    __builtin_amdgcn_sched_barrier(0);
+    // stage 3 for b: products -> LDS (branch-free); vC / gC die here, so
+    // the next stages' registers reuse them (peak ~ one block in flight)
+    {
+      const int ka = k0 & ~1;
+      const int lim = min(cnt, TL::cap);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pos = 2 * (t + u * kBlock) + ka - k0;
+        const int q0 = (pos >= 0 && pos < lim) ? pos : TL::tile;
+        const int q1 = (pos + 1 >= 0 && pos + 1 < lim) ? pos + 1 : TL::tile + 1;
+        sm.prod[q0] = vC[u].x * gC0[u];
+        sm.prod[q1] = vC[u].y * gC1[u];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // stage 2 for b1: gathers + values; stage 1 for b2: column indices
+    gather(cN, gC0, gC1);
+    load_v(k0n, k1n, vC);
+    __builtin_amdgcn_sched_barrier(0);
+    load_c(k0nn, k1nn, cN);
+    __builtin_amdgcn_sched_barrier(0);
+    if (cnt <= TL::cap) {
+      __syncthreads();
+      if (t < nrows) {
+        T s = T(0);
+        for (int j = a; j < e; ++j) s += sm.prod[j];
+        epi.row(r0 + t, s);
+      }
+      __syncthreads();
+    } else {
+      // one row longer than a tile
+      __syncthreads();
+      T s[1] = {T(0)};
+      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x(A.col[k0 + k]);
+      block_sum<T, 1>(s, sm.red);
+      if (t == 0) epi.row(r0, s[0]);
+      __syncthreads();
+    }
+    if (!has_next) break;
+    b = nb;
+    r0 = A.rb[b];
+    r1 = A.rb[b + 1];
+    k0 = k0n;
+    k1 = k1n;
+    b1 = b2;
+    k0n = k0nn;
+    k1n = k1nn;
+  }
+}
+
+// Quad form of the pipelined loop (variant bit 256): the vector-memory
+// pipeline (TA/TD) is the measured bottleneck (profiles/r01_pmc_spmv.txt:
+// TA_TA_BUSY ~90 % of kernel cycles), so this form issues fewer memory
+// instructions per row block: val as two 16-B loads and col as one 16-B load
+// per 4 entries (pairs: 16-B + 8-B per 2 entries), and one row-pointer load
+// per row (the next row's start comes through LDS, the block's end from the
+// schedule) instead of two.
+template <typename T> struct QuadOf;
+template <> struct QuadOf<double> { typedef double V __attribute__((ext_vector_type(4))); };
+template <> struct QuadOf<float> { typedef float V __attribute__((ext_vector_type(4))); };
+typedef int Int4 __attribute__((ext_vector_type(4)));
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__restrict__ val,
+                                               const Gather &x, Epi &epi,
+                                               SpmvLds<T, TileOf<V>::tile> &sm) {
+  using TL = TileOf<V>;
+  constexpr bool NT = (V & 2) != 0;
+  using QV = typename QuadOf<T>::V;
+  constexpr int U = TL::tile / (4 * kBlock);
+  constexpr int CAP = TL::tile - 6;  // quads read up to 6 extra entries
+  const int t = threadIdx.x;
+  int b, step, end;
+  work_range<V>(A.nrb, b, step, end);
+  if (b >= end) return;
+  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  QV v[U];
+  Int4 c[U];
+  auto issue = [&](int kk0, int kk1, QV(&vv)[U], Int4(&cc)[U]) {
+    const bool ok = kk1 > kk0;  // empty blocks read quad [0, 4) (nnz >= 4)
+    const int ka = ok ? (kk0 & ~3) : 0;
+    const int nq = ok ? ((kk1 - ka + 3) >> 2) : 1;
+    const QV *v4 = reinterpret_cast<const QV *>(val + ka);
+    const Int4 *c4 = reinterpret_cast<const Int4 *>(A.col + ka);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(t + u * kBlock, nq - 1);
+      vv[u] = ldg<NT>(v4 + j);
+      cc[u] = ldg<NT>(c4 + j);
+    }
+  };
+  issue(k0, k1, v, c);
+  for (;;) {
+    const int nb = b + step;
+    const bool has_next = nb < end;
+    const int nbb = has_next ? nb : b;
+    const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
+    const int nrows = r1 - r0, cnt = k1 - k0;
+    const int tr = min(t, max(nrows - 1, 0));
+    const int rpt = A.rowptr[r0 + tr];
+    epi.pre(r0 + tr);
+    T g[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g[u][0] = x(c[u].x);
+      g[u][1] = x(c[u].y);
+      g[u][2] = x(c[u].z);
+      g[u][3] = x(c[u].w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    QV vn[U];
+    Int4 cn[U];
+    issue(nk0, nk1, vn, cn);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int ka = k0 & ~3;
+      const int lim = min(cnt, CAP);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pos = 4 * (t + u * kBlock) + ka - k0;
+        const T vq[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int pq = pos + q;
+          const int dst = (pq >= 0 && pq < lim) ? pq : TL::tile + q;
+          sm.prod[dst] = vq[q] * g[u][q];
+        }
+      }
+      if (t < nrows) sm.rp[t] = rpt;
+      if (t == 0) sm.rp[nrows] = k1;
+    }
+    if (cnt <= CAP) {
+      __syncthreads();
+      if (t < nrows) {
+        const int a = sm.rp[t] - k0, e = sm.rp[t + 1] - k0;
+        T s = T(0);
+        for (int j = a; j < e; ++j) s += sm.prod[j];
+        epi.row(r0 + t, s);
+      }
+      __syncthreads();
+    } else {
+      // one row longer than a tile
+      __syncthreads();
+      T s[1] = {T(0)};
+      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x(A.col[k0 + k]);
       block_sum<T, 1>(s, sm.red);
       if (t == 0) epi.row(r0, s[0]);
       __syncthreads();
@@ -362,11 +634,134 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
   }
 }
 
-template <typename T, int V, class Epi>
+// Wave tiles (variant bit 512): every wave owns its row blocks (<= 64 rows,
+// <= 506 entries; schedule tile 512), stages its products in its own LDS
+// slice and sums its rows without any workgroup barrier — LDS operations of
+// one wave complete in order, so a wave-level compiler fence is enough. Same
+// one-ahead pipeline as spmv_rows_pipe (paired loads). Rows longer than a
+// wave tile are summed by the whole wave (tree order).
+template <typename T> struct WaveLds {
+  T prod[4][512 + 4];  // per wave: tile + 4 scratch slots
+  T red[4 * kMaxRed];
+  int flag;
+  int rp[1];  // unused (keeps the SpmvLds member set)
+};
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_waves(const CsrArgs &A, const T *__restrict__ val,
+                                           const Gather &x, Epi &epi, WaveLds<T> &sm) {
+  constexpr bool NT = (V & 2) != 0;
+  using PV = typename PairOf<T>::V;
+  constexpr int WT = 512, CAP = WT - 6, U = WT / (2 * 64);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  T *prod = sm.prod[w];
+  const int G = gridDim.x;
+  int b, step, end;
+  if ((V & 1) && (G & 7) == 0) {
+    const int g = blockIdx.x & 7;
+    b = (int)(((int64_t)A.nrb * g) >> 3) + (blockIdx.x >> 3) * 4 + w;
+    end = (int)(((int64_t)A.nrb * (g + 1)) >> 3);
+    step = (G >> 3) * 4;
+  } else {
+    b = blockIdx.x * 4 + w;
+    step = G * 4;
+    end = A.nrb;
+  }
+  if (b >= end) return;
+  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  PV v[U];
+  Int2 c[U];
+  auto issue = [&](int kk0, int kk1, PV(&vv)[U], Int2(&cc)[U]) {
+    const bool ok = kk1 > kk0;
+    const int ka = ok ? (kk0 & ~1) : 0;
+    const int np = ok ? ((kk1 - ka + 1) >> 1) : 1;
+    const PV *v2 = reinterpret_cast<const PV *>(val + ka);
+    const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(lane + u * 64, np - 1);
+      vv[u] = ldg<NT>(v2 + j);
+      cc[u] = ldg<NT>(c2 + j);
+    }
+  };
+  issue(k0, k1, v, c);
+  for (;;) {
+    const int nb = b + step;
+    const bool has_next = nb < end;
+    const int nbb = has_next ? nb : b;
+    const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
+    const int nrows = r1 - r0, cnt = k1 - k0;
+    const int tr = min(lane, max(nrows - 1, 0));
+    const int rpt = A.rowptr[r0 + tr];
+    epi.pre(r0 + tr);
+    T g0[U], g1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g0[u] = x(c[u].x);
+      g1[u] = x(c[u].y);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    PV vn[U];
+    Int2 cn[U];
+    issue(nk0, nk1, vn, cn);
+    __builtin_amdgcn_sched_barrier(0);
+    if (cnt <= CAP) {
+      const int ka = k0 & ~1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pos = 2 * (lane + u * 64) + ka - k0;
+        const int q0 = (pos >= 0 && pos < cnt) ? pos : WT;
+        const int q1 = (pos + 1 >= 0 && pos + 1 < cnt) ? pos + 1 : WT + 1;
+        prod[q0] = v[u].x * g0[u];
+        prod[q1] = v[u].y * g1[u];
+      }
+      // end of row `lane`: the next lane's start, or the block's end
+      const int nxt = __shfl_down(rpt, 1, 64);
+      const int rend = (lane + 1 < nrows) ? nxt : k1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < nrows) {
+        T s = T(0);
+        for (int j = rpt - k0; j < rend - k0; ++j) s += prod[j];
+        epi.row(r0 + lane, s);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      // one row longer than a wave tile: the whole wave sums it
+      T s = T(0);
+      for (int kk = lane; kk < cnt; kk += 64) s += val[k0 + kk] * x(A.col[k0 + kk]);
+      s = wave_sum(s);
+      if (lane == 0) epi.row(r0, s);
+    }
+    if (!has_next) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = vn[u];
+      c[u] = cn[u];
+    }
+    b = nb;
+    r0 = nr0;
+    r1 = nr1;
+    k0 = nk0;
+    k1 = nk1;
+  }
+}
+
+// LDS layout of a variant's kernel
+template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
+template <typename T, int V>
+using LdsOf = typename std::conditional<(V & 512) != 0, WaveLds<T>,
+                                        SpmvLds<T, TileOf<V>::tile>>::type;
+
+template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
-                                         const T *__restrict__ x, Epi &epi, SpmvLds<T> &sm) {
-  if constexpr ((V & 8) != 0) spmv_rows_pipe<T, V, Epi>(A, val, x, epi, sm);
-  else spmv_rows<T, V, Epi>(A, val, x, epi, sm);
+                                         const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
+  if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
+  else if constexpr ((V & 256) != 0) spmv_rows_quad<T, V, Epi, Gather>(A, val, x, epi, sm);
+  else if constexpr ((V & 128) != 0) spmv_rows_deep<T, V, Epi, Gather>(A, val, x, epi, sm);
+  else if constexpr ((V & 8) != 0) spmv_rows_pipe<T, V, Epi, Gather>(A, val, x, epi, sm);
+  else spmv_rows<T, V, Epi, Gather>(A, val, x, epi, sm);
 }
 
 // Row epilogues: pre(i) loads the row's own operands early (the pipelined
@@ -400,6 +795,31 @@ template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
     acc += ri * ri;
   }
 };
+// Fused iteration k: p_k = r_k + beta_{k-1} p_{k-1} (CG.hpp:418 of body
+// k-1), x += alpha_{k-1} p_{k-1} (CG.hpp:390 of body k-1, deferred), then
+// helper = A p_k and value2 += helper.p_k (CG.hpp:374-379 of body k).
+template <typename T> struct EpiFused {
+  const T *__restrict__ r;
+  const T *__restrict__ pp;  // p_{k-1}
+  T *__restrict__ pc;        // p_k
+  T *__restrict__ x;
+  T *__restrict__ Ap;
+  T alpha, beta;
+  bool do_x;
+  T acc, rv, pv, xv;
+  __device__ __forceinline__ void pre(int i) {
+    rv = r[i];
+    pv = pp[i];
+    xv = x[i];
+  }
+  __device__ __forceinline__ void row(int i, T s) {
+    const T pi = rv + beta * pv;
+    pc[i] = pi;
+    Ap[i] = s;
+    acc += s * pi;
+    if (do_x) x[i] = xv + alpha * pv;
+  }
+};
 template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
@@ -418,9 +838,9 @@ template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_spmv(CsrArgs A, const T *__restrict__ val,
                                                  const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ SpmvLds<T> sm;
+  __shared__ LdsOf<T, V> sm;
   EpiStore<T> e{y};
-  spmv_any<T, V>(A, val, x, e, sm);
+  spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
 }
 
 template <typename T, int V>
@@ -429,9 +849,9 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
                                                     const T *__restrict__ b, T *__restrict__ r,
                                                     T *__restrict__ p, CgScalars<T> *st,
                                                     RedWs<T> *ws, T tol, long long cap) {
-  __shared__ SpmvLds<T> sm;
+  __shared__ LdsOf<T, V> sm;
   EpiInit<T> e{b, r, p, T(0), T(0)};
-  spmv_any<T, V>(A, val, x, e, sm);
+  spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
     st->rxr[0] = v[0];
@@ -439,6 +859,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
     st->tol = tol;
     st->active[0] = 1;
     st->active[1] = st->active[2] = st->active[3] = 0;
+    st->xpend[0] = st->xpend[1] = st->xpend[2] = st->xpend[3] = 0;
     st->bodies = 0;
     st->cap = cap;
     st->stopped = 0;
@@ -451,11 +872,63 @@ __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restr
                                                      T *__restrict__ Ap, CgScalars<T> *st,
                                                      int slot, RedWs<T> *ws) {
   if (!st->active[slot]) return;
-  __shared__ SpmvLds<T> sm;
+  __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0)};
-  spmv_any<T, V>(A, val, p, e, sm);
+  spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) st->pAp[slot] = v[0];
+}
+
+// Fused iteration, kernel 1 of 2 (slot s of body k). Reads active[s] (run
+// body k), xpend[s-1] (the x update of body k-1 is still pending) and
+// bodies == 0 (body 0: p_{-1} = 0, beta = 0). With body k inactive it only
+// applies the pending x update. The last workgroup publishes p.Ap and clears
+// xpend[s-1].
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock) void k_spmv_fused(CsrArgs A, const T *__restrict__ val,
+                                                       const T *__restrict__ r,
+                                                       const T *__restrict__ pp,
+                                                       T *__restrict__ pc, T *__restrict__ x,
+                                                       T *__restrict__ Ap, CgScalars<T> *st,
+                                                       int slot, RedWs<T> *ws) {
+  const int prev = (slot + 3) & 3;
+  const bool act = st->active[slot] != 0;
+  const bool xp = st->xpend[prev] != 0;
+  if (!act && !xp) return;
+  __shared__ LdsOf<T, V> sm;
+  const T alpha = xp ? st->rxr[prev] / st->pAp[prev] : T(0);
+  T v[1] = {T(0)};
+  if (act) {
+    const T beta = st->bodies == 0 ? T(0) : st->rr[prev] / st->rxr[prev];
+    EpiFused<T> e{r, pp, pc, x, Ap, alpha, beta, xp, T(0), T(0), T(0), T(0)};
+    spmv_any<T, V>(A, val, GatherP<T>{r, pp, beta}, e, sm);
+    v[0] = e.acc;
+  } else {
+    // stopped after body k-1: only its deferred x update remains
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n; i += stride)
+      x[i] = x[i] + alpha * pp[i];
+  }
+  if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
+    if (act) st->pAp[slot] = v[0];
+    if (xp) st->xpend[prev] = 0;
+  }
+}
+
+// Apply a pending x update (end of a run of fused iterations): x += alpha p.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_flush_x(int64_t n, T *__restrict__ x,
+                                                    const T *__restrict__ p, CgScalars<T> *st,
+                                                    int slot, RedWs<T> *ws) {
+  if (!st->xpend[slot]) return;
+  __shared__ T red[4];
+  __shared__ int flag;
+  const T alpha = st->rxr[slot] / st->pAp[slot];
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    x[i] = x[i] + alpha * p[i];
+  T v[1] = {T(0)};
+  if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) st->xpend[slot] = 0;
 }
 
 template <typename T, int V>
@@ -463,9 +936,9 @@ __global__ __launch_bounds__(kBlock) void k_accuracy(CsrArgs A, const T *__restr
                                                      const T *__restrict__ b,
                                                      const T *__restrict__ x, T *out2,
                                                      RedWs<T> *ws) {
-  __shared__ SpmvLds<T> sm;
+  __shared__ LdsOf<T, V> sm;
   EpiAccuracy<T> e{b, x, T(0), T(0), T(0), T(0)};
-  spmv_any<T, V>(A, val, x, e, sm);
+  spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
   T v[2] = {e.acc0, e.acc1};
   if (grid_reduce<T, 2>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
     out2[0] = v[0];
@@ -481,12 +954,17 @@ template <> struct Vec2<double> { using V = double2; };
 template <> struct Vec2<float> { using V = float2; };
 
 // r = r - alpha * Ap ; rr = r.r          (CG.hpp:381-393, 406-407)
-template <typename T>
+// FUSED: kernel 2 of 2 of the fused iteration, which also runs the stop rule
+// (CG.hpp:396-404, 410-417, 436) and marks body k's x update as pending.
+template <typename T, bool FUSED>
 __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
                                                      RedWs<T> *ws) {
-  if (!st->active[slot]) return;
+  if (!st->active[slot]) {
+    if (FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
+    return;
+  }
   __shared__ T red[4];
   __shared__ int flag;
   const T alpha = st->rxr[slot] / st->pAp[slot];
@@ -525,7 +1003,21 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
     acc += v * v;
   }
   T v[1] = {acc};
-  if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) st->rr[slot] = v[0];
+  if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) {
+    st->rr[slot] = v[0];
+    if (FUSED) {
+      const int nxt = (slot + 1) & 3;
+      const T rxr = st->rxr[slot];
+      const long long m = st->bodies + 1;
+      st->bodies = m;
+      const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
+      const bool cont = !cond && m < st->cap;
+      st->active[nxt] = cont ? 1 : 0;
+      st->rxr[nxt] = v[0];
+      st->xpend[slot] = 1;
+      st->stopped = cond ? 1 : (cont ? 0 : 2);
+    }
+  }
 }
 
 // x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
@@ -689,7 +1181,7 @@ inline int elem_grid(int64_t n, int per_thread) {
   return (int)g;
 }
 
-inline CsrArgs args(const CsrDev &A) { return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb}; }
+inline CsrArgs args(const CsrDev &A) { return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb, A.n}; }
 
 }  // namespace
 
@@ -730,11 +1222,22 @@ constexpr int kSpmvV = -1;
 constexpr int64_t kNtMinBytes = int64_t(256) << 20;
 
 template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
+  if (v < 0 && A.variant > 0) v = A.variant;  // chosen by cgx_csr_create's autotune
   if (v < 0) v = (A.nnz * int64_t(sizeof(T) + sizeof(int)) >= kNtMinBytes) ? 15 : 13;
-  v &= 15;
-  if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2) v &= ~12;
+  v &= 1023;  // bits 16/32: timing ablations, only reachable through cgx_tune_spmv
+  const int tile = A.tile == 1024 ? 64 : 0;  // the kernel tile follows the schedule
+  if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2)
+    return tile;  // plain loads, no pipelining (any schedule with <= 2042-entry blocks)
+  if (A.tile == 512) return 512 | 12 | (v & 3);  // wave tiles: 524..527
+  v &= ~512;
+  if ((v & 256) && (((uintptr_t)A.val % (4 * sizeof(T))) || ((uintptr_t)A.col % 16) ||
+                    A.nnz < 4 || tile))
+    v &= ~256;  // quads need 4-entry alignment and full tiles
+  if (v & 256) return 256 | 8 | (v & 3);  // 264..267
   if ((v & 8) && !(v & 4)) v &= ~8;  // the pipelined loop uses paired loads
-  return v;
+  if ((v & 128) && (!(v & 4) || tile)) v &= ~128;  // deep pipeline: paired, full tiles
+  if (v & 128) v |= 8;
+  return v | tile;
 }
 
 #define CGX_LAUNCH_V(KERNEL, VV, ...)                                          \
@@ -746,18 +1249,43 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 
 #define CGX_SPMV_SWITCH(v, KERNEL, ...)                                        \
   switch (v) {                                                                 \
-    case 0: CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);                              \
-    case 1: CGX_LAUNCH_V(KERNEL, 1, __VA_ARGS__);                              \
-    case 2: CGX_LAUNCH_V(KERNEL, 2, __VA_ARGS__);                              \
-    case 3: CGX_LAUNCH_V(KERNEL, 3, __VA_ARGS__);                              \
-    case 4: CGX_LAUNCH_V(KERNEL, 4, __VA_ARGS__);                              \
-    case 5: CGX_LAUNCH_V(KERNEL, 5, __VA_ARGS__);                              \
-    case 6: CGX_LAUNCH_V(KERNEL, 6, __VA_ARGS__);                              \
-    case 7: CGX_LAUNCH_V(KERNEL, 7, __VA_ARGS__);                              \
-    case 12: CGX_LAUNCH_V(KERNEL, 12, __VA_ARGS__);                            \
-    case 13: CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);                            \
-    case 14: CGX_LAUNCH_V(KERNEL, 14, __VA_ARGS__);                            \
-    default: CGX_LAUNCH_V(KERNEL, 15, __VA_ARGS__);                            \
+    case 0: CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);                                      \
+    case 1: CGX_LAUNCH_V(KERNEL, 1, __VA_ARGS__);                                      \
+    case 2: CGX_LAUNCH_V(KERNEL, 2, __VA_ARGS__);                                      \
+    case 3: CGX_LAUNCH_V(KERNEL, 3, __VA_ARGS__);                                      \
+    case 4: CGX_LAUNCH_V(KERNEL, 4, __VA_ARGS__);                                      \
+    case 5: CGX_LAUNCH_V(KERNEL, 5, __VA_ARGS__);                                      \
+    case 6: CGX_LAUNCH_V(KERNEL, 6, __VA_ARGS__);                                      \
+    case 7: CGX_LAUNCH_V(KERNEL, 7, __VA_ARGS__);                                      \
+    case 12: CGX_LAUNCH_V(KERNEL, 12, __VA_ARGS__);                                    \
+    case 13: CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);                                    \
+    case 14: CGX_LAUNCH_V(KERNEL, 14, __VA_ARGS__);                                    \
+    case 15: CGX_LAUNCH_V(KERNEL, 15, __VA_ARGS__);                                    \
+    case 64: CGX_LAUNCH_V(KERNEL, 64, __VA_ARGS__);                                    \
+    case 65: CGX_LAUNCH_V(KERNEL, 65, __VA_ARGS__);                                    \
+    case 66: CGX_LAUNCH_V(KERNEL, 66, __VA_ARGS__);                                    \
+    case 67: CGX_LAUNCH_V(KERNEL, 67, __VA_ARGS__);                                    \
+    case 68: CGX_LAUNCH_V(KERNEL, 68, __VA_ARGS__);                                    \
+    case 69: CGX_LAUNCH_V(KERNEL, 69, __VA_ARGS__);                                    \
+    case 70: CGX_LAUNCH_V(KERNEL, 70, __VA_ARGS__);                                    \
+    case 71: CGX_LAUNCH_V(KERNEL, 71, __VA_ARGS__);                                    \
+    case 524: CGX_LAUNCH_V(KERNEL, 524, __VA_ARGS__);                                 \
+    case 525: CGX_LAUNCH_V(KERNEL, 525, __VA_ARGS__);                                 \
+    case 526: CGX_LAUNCH_V(KERNEL, 526, __VA_ARGS__);                                 \
+    case 527: CGX_LAUNCH_V(KERNEL, 527, __VA_ARGS__);                                 \
+    case 264: CGX_LAUNCH_V(KERNEL, 264, __VA_ARGS__);                                 \
+    case 265: CGX_LAUNCH_V(KERNEL, 265, __VA_ARGS__);                                 \
+    case 266: CGX_LAUNCH_V(KERNEL, 266, __VA_ARGS__);                                 \
+    case 267: CGX_LAUNCH_V(KERNEL, 267, __VA_ARGS__);                                 \
+    case 140: CGX_LAUNCH_V(KERNEL, 140, __VA_ARGS__);                                 \
+    case 141: CGX_LAUNCH_V(KERNEL, 141, __VA_ARGS__);                                 \
+    case 142: CGX_LAUNCH_V(KERNEL, 142, __VA_ARGS__);                                 \
+    case 143: CGX_LAUNCH_V(KERNEL, 143, __VA_ARGS__);                                 \
+    case 76: CGX_LAUNCH_V(KERNEL, 76, __VA_ARGS__);                                    \
+    case 77: CGX_LAUNCH_V(KERNEL, 77, __VA_ARGS__);                                    \
+    case 78: CGX_LAUNCH_V(KERNEL, 78, __VA_ARGS__);                                    \
+    case 79: CGX_LAUNCH_V(KERNEL, 79, __VA_ARGS__);                                    \
+    default: return hipErrorInvalidValue;                                      \
   }
 
 template <typename T>
@@ -780,13 +1308,37 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                        CgScalars<T> *st, RedWs<T> *ws, hipStream_t s) {
-  CGX_SPMV_SWITCH(spmv_variant<T>(A, v), k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0,
-                  ws);
+  const int vv = spmv_variant<T>(A, v);
+  switch (vv) {  // timing ablations (bits 16/32) exist for this kernel only
+    case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 63: CGX_LAUNCH_V(k_spmv_dot, 63, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    default: break;
+  }
+  CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
 }
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                               RedWs<T> *ws, hipStream_t s) {
-  CGX_LAUNCH(k_update_r<T>, grid_elems(n), n, r, Ap, st, slot, ws);
+                               RedWs<T> *ws, hipStream_t s, bool fused) {
+  if (fused) {
+    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
+                       st, slot, ws);
+  } else {
+    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
+                       st, slot, ws);
+  }
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t Launch<T>::spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
+                                 CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s) {
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_fused, args(A), (const T *)A.val, r, pp, pc, x, Ap,
+                  st, slot, ws);
+}
+template <typename T>
+hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,
+                              RedWs<T> *ws, hipStream_t s) {
+  CGX_LAUNCH(k_flush_x<T>, elem_grid(n, 4), n, x, p, st, slot, ws);
 }
 template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,

@@ -91,6 +91,8 @@ struct cgx_cg {
   int dtype = CGX_F64;
   int64_t n = 0;
   void *r = nullptr, *p = nullptr, *Ap = nullptr;  // p, Ap: n + n_ghost
+  void *p2 = nullptr;   // second p buffer of the fused iteration (single device)
+  bool fused = false;   // two kernels per iteration (x/p update folded into SpMV)
   void *st = nullptr;   // cgx::CgScalars<T>
   void *ws = nullptr;   // cgx::RedWs<T>
   const void *b = nullptr;

@@ -72,6 +72,12 @@ int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d_rowptr,
 int cgx_csr_destroy(cgx_csr *csr);
 int cgx_csr_info(cgx_csr *csr, int64_t *n, int64_t *nnz, int64_t *row_blocks,
                  int *max_row_nnz);
+/* Rebuild the SpMV schedule for row blocks of `tile` entries (2048, the
+ * default, or 1024 with at most 128 rows). Blocking. */
+int cgx_csr_set_tile(cgx_csr *csr, int tile);
+/* SpMV variant cgx_csr_create picked for this matrix by timing the candidate
+ * kernels on the device ($CGX_SPMV_VARIANT overrides; 0 = size heuristic). */
+int cgx_csr_variant(cgx_csr *csr, int *variant);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
  * Scalars are DEVICE pointers, as in the reference (Scalar<DT>::ptr()). */
@@ -119,6 +125,13 @@ int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable);
 int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
 /* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
 int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
+/* Iteration structure (before cgx_cg_begin): 0 auto (= 1), 1 three kernels
+ * (SpMV+p.Ap, r-update+r.r, x/p-update), 2 fused (single device only): two
+ * kernels, the x/p update folded into the next iteration's SpMV (p_j =
+ * r_j + beta p_old_j computed in the gather), 8 bytes/row less traffic but
+ * twice the gathers; measured no faster on MI355X. Both modes
+ * give bit-identical x. */
+int cgx_cg_set_mode(cgx_cg *cg, int mode);
 
 /* CG::accuracy (CG.hpp:463-515): blocking; |sum (b-Ax)^2 / sum x^2|. */
 int cgx_accuracy(cgx_ctx *ctx, cgx_csr *A, const void *d_b, const void *d_x,

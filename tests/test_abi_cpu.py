@@ -80,7 +80,7 @@ def test_row_block_schedule(oracle, case):
     for a, b in zip(rb[:-1], rb[1:]):
         cnt = rp[b] - rp[a]
         assert b - a <= 256
-        assert cnt <= 2046 or b - a == 1      # a long row is alone
+        assert cnt <= 2042 or b - a == 1      # a long row is alone
     if case == "poisson":
         assert np.all(np.diff(rb)[:-1] == 256)  # 7-nnz rows fill whole blocks
 

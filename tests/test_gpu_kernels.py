@@ -197,3 +197,67 @@ def test_errors(queue):
     cg.setTarget(np.ones(4))
     with pytest.raises(RuntimeError, match="No Matrix"):
         cg.solve(1e-8)
+
+
+def _run_modes(rp, cl, vl, b, tol, max_iter=-1, poll=32, graph=True):
+    out = {}
+    for mode in (1, 2):
+        cg = cga.CG.createCG()
+        cg.mode = mode
+        cg.poll_every = poll
+        cg.use_graph = graph
+        cg.setMatrix(vl, cl, rp)
+        cg.setTarget(b)
+        cg.solve(tol, max_iter=max_iter)
+        out[mode] = (cg.extract(), cg.iterations, cg.final_rxr)
+    return out
+
+
+@pytest.mark.parametrize("case,tol,poll,graph", [("p2d", 1e-8, 32, True), ("p3d", 1e-24, 8, False),
+                                                  ("irr", 1e-6, 4, True), ("p2d", 0.0, 32, True)])
+def test_fused_iteration_bit_identical_to_three_kernels(oracle, case, tol, poll, graph):
+    """Mode 2 folds the x/p update into the next SpMV; every value it computes
+    is the same expression as mode 1's, so x is bit-identical."""
+    if case == "p2d":
+        rp, cl, vl = oracle.poisson(2, 48, 40, 1)
+    elif case == "p3d":
+        rp, cl, vl = oracle.poisson(3, 12, 11, 10)
+    else:
+        rp, cl, vl = irregular_spd(20_000, seed=4)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    out = _run_modes(rp, cl, vl, b, tol, poll=poll, graph=graph)
+    (x1, it1, r1), (x2, it2, r2) = out[1], out[2]
+    assert it1 == it2
+    np.testing.assert_array_equal(x1, x2)
+    assert r1 == r2 or (np.isnan(r1) and np.isnan(r2))
+
+
+def test_fused_split_runs(queue, oracle):
+    """begin + several cgx_cg_run calls (each ends with the pending-x flush)
+    equals one run, and the oracle capped at the same count."""
+    import ctypes as C
+    from conjugategradient_amd._native import check, lib
+    rp, cl, vl = oracle.poisson(2, 30, 30, 1)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)
+    A = Matrix(queue, vl, cl, rp)
+    bv = Vector(queue, b)
+    L = lib()
+    xs = {}
+    for split in ((23,), (5, 1, 17), (7, 16)):
+        xv = Vector(queue, n)
+        h = C.c_void_p()
+        check(L.cgx_cg_create(queue.handle, A.schedule(), C.byref(h)))
+        check(L.cgx_cg_set_mode(h, 2))
+        check(L.cgx_cg_config(h, 4, 1))
+        check(L.cgx_cg_begin(h, bv.ptr(), xv.ptr(), 0.0, 1000))
+        tot, st = C.c_int64(), C.c_int()
+        for k in split:
+            check(L.cgx_cg_run(h, k, C.byref(tot), C.byref(st)))
+        assert tot.value == 23
+        xs[split] = xv.to_numpy()
+        L.cgx_cg_destroy(h)
+    xr, res = oracle.cg_solve(rp, cl, vl, b, 0.0, max_iter=23)
+    for x in xs.values():
+        np.testing.assert_array_equal(x, xs[(23,)])
+    assert rel(xs[(23,)], xr) <= 1e-12

@@ -14,7 +14,7 @@ fi
 BENCH="bench.py --steps 50 --warmup 5 --no-cpu"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH > $OUT/bench_trace.log 2>&1 || { echo TRACE_FAIL; tail -20 $OUT/bench_trace.log; exit 1; }
 tail -1 $OUT/bench_trace.log
-PBENCH="bench.py --steps 10 --warmup 2 --no-cpu --no-kernel-timing"
+PBENCH="bench.py --steps 10 --warmup 2 --no-cpu --profile-steps 0"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 $PBENCH > $OUT/pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; tail -20 $OUT/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 $PBENCH > $OUT/pmc_write.log 2>&1 || { echo PMC_WRITE_FAIL; tail -20 $OUT/pmc_write.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc_hit -o run --output-format csv -- python3 $PBENCH > $OUT/pmc_hit.log 2>&1 || { echo PMC_HIT_FAIL; tail -20 $OUT/pmc_hit.log; exit 1; }

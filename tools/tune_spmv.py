@@ -50,13 +50,23 @@ def main():
     for name in a.configs.split(","):
         A = matrix(q, name)
         n, nnz = A.N(), A.NNZ()
+        # a second schedule with half tiles for the variants with bit 64
+        half = C.c_void_p()
+        check(L.cgx_csr_create(q.handle, n, nnz, A.rows().ptr, A.columns().ptr, A.data().ptr, 0,
+                               None, C.byref(half)))
+        check(L.cgx_csr_set_tile(half, 1024))
+        wave = C.c_void_p()  # wave tiles for the variants with bit 512
+        check(L.cgx_csr_create(q.handle, n, nnz, A.rows().ptr, A.columns().ptr, A.data().ptr, 0,
+                               None, C.byref(wave)))
+        check(L.cgx_csr_set_tile(wave, 512))
         x = cga.Vector(q, np.random.default_rng(0).standard_normal(n))
         ys = {v: cga.Vector(q, n) for v in variants}
         times = {v: [] for v in variants}
         for _ in range(a.rounds):
             for v in variants:
                 ms = C.c_double(0)
-                check(L.cgx_tune_spmv(q.handle, A.schedule(), v, x.ptr(), ys[v].ptr(), a.iters,
+                sched = wave if v & 512 else half if v & 64 else A.schedule()
+                check(L.cgx_tune_spmv(q.handle, sched, v, x.ptr(), ys[v].ptr(), a.iters,
                                       C.byref(ms)))
                 times[v].append(ms.value)
         y0 = ys[variants[0]].to_numpy()
@@ -69,6 +79,8 @@ def main():
                               "min_us": round(float(t.min()), 2),
                               "GBps_median": round(nbytes / (np.median(t) * 1e-6) / 1e9, 1),
                               "bitexact_vs_v0": same}), flush=True)
+        L.cgx_csr_destroy(half)
+        L.cgx_csr_destroy(wave)
         del A, x, ys
 
 
