@@ -20,7 +20,8 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcgx.so")
+# CGX_LIB selects another build of the same library (A/B measurements).
+LIB_PATH = os.environ.get("CGX_LIB") or os.path.join(HERE, "libcgx.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "cgx.h")
 
 F64, F32 = 0, 1
@@ -59,6 +60,8 @@ _SIGS = {
     "cgx_csr_destroy": (_i32, [_vp]),
     "cgx_csr_set_tile": (_i32, [_vp, _i32]),
     "cgx_csr_variant": (_i32, [_vp, C.POINTER(_i32)]),
+    "cgx_csr_set_variant": (_i32, [_vp, _i32]),
+    "cgx_csr_sell_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(C.c_int64)]),
     "cgx_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
                             C.POINTER(_i32)]),
     "cgx_spmv": (_i32, [_vp, _vp, _vp, _vp, _i64]),
@@ -94,6 +97,9 @@ _SIGS = {
                                C.POINTER(C.POINTER(_i64)), _vp]),
     "cgx_plan_remap": (_i32, [_i64, _i64, _i64, _vp, _i64, _vp]),
     "cgx_free_host": (None, [_vp]),
+    "cgx_sell_plan": (_i32, [_vp, _vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
+                             C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
+                             C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(_i64)]),
     "cgx_tune_spmv": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, C.POINTER(_dbl)]),
     "cgx_row_blocks": (_i32, [_vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i32)),
                               C.POINTER(_i32)]),

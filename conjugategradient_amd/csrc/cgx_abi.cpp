@@ -389,6 +389,8 @@ extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
 }
 
 int autotune_spmv(cgx_csr *A);
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col);
+void free_sell(cgx_csr *A);
 
 // ===========================================================================
 // CSR
@@ -444,7 +446,8 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   A->dev.rb = A->d_rb;
   A->dev.rbk = A->d_rb + nrb1;
   A->n_global = n;
-  int rc = autotune_spmv(A);
+  int rc = build_sell(A, h_rowptr, nullptr);
+  if (!rc) rc = autotune_spmv(A);
   if (rc) {
     cgx_csr_destroy(A);
     return rc;
@@ -459,6 +462,7 @@ extern "C" int cgx_csr_destroy(cgx_csr *A) {
   (void)hipStreamSynchronize(A->ctx->stream);
   if (A->d_rb) (void)hipFree(A->d_rb);
   if (A->d_ext) (void)hipFree(A->d_ext);
+  free_sell(A);
   dist_destroy_halo(A);
   delete A;
   return CGX_OK;
@@ -510,18 +514,235 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
   return CGX_OK;
 }
 
+void free_sell(cgx_csr *A) {
+  for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  A->dev.sl = nullptr;
+  A->dev.sdict = nullptr;
+  A->dev.sidx = nullptr;
+  A->dev.sval = nullptr;
+  A->dev.nsl = 0;
+  A->dev.sell_maxw = 0;
+  A->sell_padded = 0;
+}
+
+// SELL-64 layout of a host CSR (cgx_internal.h SellSlice; DESIGN.md §SpMV
+// formats). Qualifies when every 64-row slice has rows of at most
+// kSellMaxWidth entries and at most kSellMaxDict distinct (col - row)
+// offsets, and the padding adds at most a quarter of the entries (+4096) — stencil
+// and other banded matrices. Returns false (outputs unspecified) otherwise.
+// voff_total: value slots of the layout (the kernel reads one chunk beyond).
+static bool sell_plan_host(int64_t n, const int *rowptr, const int *col,
+                           std::vector<SellSlice> &sl, std::vector<int> &pool,
+                           std::vector<unsigned long long> &idx, int64_t &voff_total) {
+  const int64_t nnz = (int64_t)rowptr[n] - rowptr[0];
+  if (nnz < 1 || n + kSellRows >= (int64_t(1) << 31)) return false;
+  const int64_t nsl = (n + kSellRows - 1) / kSellRows;
+  sl.assign((size_t)nsl, SellSlice{});
+  int64_t voff = 0, ioff = 0, padded = 0;
+  for (int64_t q = 0; q < nsl; ++q) {
+    const int64_t r0 = q * kSellRows, r1 = std::min(n, r0 + kSellRows);
+    int w = 0;
+    for (int64_t i = r0; i < r1; ++i) w = std::max(w, rowptr[i + 1] - rowptr[i]);
+    if (w > kSellMaxWidth) return false;
+    sl[(size_t)q] = SellSlice{voff, ioff, 0, w};
+    voff += (int64_t)kSellRows * w;
+    ioff += (int64_t)kSellRows * ((w + 7) / 8);
+    padded += (r1 - r0) * w;
+  }
+  if (padded > nnz + nnz / 4 + 4096) return false;  // small matrices: padding is noise
+  // per-slice dictionaries (first-seen order), shared between equal slices
+  pool.clear();
+  std::vector<std::pair<std::vector<int>, int>> seen;  // recent distinct dictionaries
+  idx.assign((size_t)ioff, ~0ull);
+  std::vector<int> d;
+  d.reserve(kSellMaxDict);
+  for (int64_t q = 0; q < nsl; ++q) {
+    SellSlice &m = sl[(size_t)q];
+    const int64_t r0 = q * kSellRows, r1 = std::min(n, r0 + kSellRows);
+    d.clear();
+    for (int64_t i = r0; i < r1; ++i) {
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const int off = col[k] - (int)i;
+        size_t t = 0;
+        while (t < d.size() && d[t] != off) ++t;
+        if (t == d.size()) {
+          if (d.size() == (size_t)kSellMaxDict) return false;
+          d.push_back(off);
+        }
+        const int j = k - rowptr[i];
+        unsigned long long &wd = idx[(size_t)(m.ioff + (int64_t)(j >> 3) * kSellRows + (i - r0))];
+        const int sh = 8 * (j & 7);
+        wd = (wd & ~(0xffull << sh)) | ((unsigned long long)t << sh);
+      }
+    }
+    int base = -1;
+    for (auto &e : seen)
+      if (e.first == d) {
+        base = e.second;
+        break;
+      }
+    if (base < 0) {
+      base = (int)pool.size();
+      pool.insert(pool.end(), d.begin(), d.end());
+      if (seen.size() >= 16) seen.erase(seen.begin());
+      seen.emplace_back(d, base);
+    }
+    m.dict = base;
+  }
+  pool.resize(pool.size() + kSellMaxDict, 0);  // every lane of the last dictionary reads in bounds
+  voff_total = voff;
+  return true;
+}
+
+extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+                             int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,
+                             unsigned long long **idx, int64_t *value_slots) {
+  CGX_REQUIRE(h_rowptr && h_col && nsl && slices && ndict && dict && nidx && idx && value_slots,
+              CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(n >= 1, CGX_EINVAL, "n=%lld", (long long)n);
+  std::vector<SellSlice> sl;
+  std::vector<int> pool;
+  std::vector<unsigned long long> ix;
+  int64_t voff = 0;
+  *nsl = *ndict = *nidx = *value_slots = 0;
+  *slices = nullptr;
+  *dict = nullptr;
+  *idx = nullptr;
+  if (!sell_plan_host(n, h_rowptr, h_col, sl, pool, ix, voff)) return CGX_OK;
+  *slices = (int64_t *)std::malloc(std::max<size_t>(sl.size(), 1) * 4 * sizeof(int64_t));
+  *dict = (int *)std::malloc(pool.size() * sizeof(int));
+  *idx = (unsigned long long *)std::malloc(std::max<size_t>(ix.size(), 1) * 8);
+  CGX_REQUIRE(*slices && *dict && *idx, CGX_ENOMEM, "host allocation failed");
+  for (size_t q = 0; q < sl.size(); ++q) {
+    (*slices)[4 * q] = sl[q].voff;
+    (*slices)[4 * q + 1] = sl[q].ioff;
+    (*slices)[4 * q + 2] = sl[q].dict;
+    (*slices)[4 * q + 3] = sl[q].width;
+  }
+  std::memcpy(*dict, pool.data(), pool.size() * sizeof(int));
+  if (!ix.empty()) std::memcpy(*idx, ix.data(), ix.size() * 8);
+  *nsl = (int64_t)sl.size();
+  *ndict = (int64_t)pool.size();
+  *nidx = (int64_t)ix.size();
+  *value_slots = voff;
+  return CGX_OK;
+}
+
+// SELL-64 copy of A on the device, when the matrix qualifies (sell_plan_host);
+// otherwise A keeps only the CSR-stream schedule and this returns CGX_OK.
+// Errors are device failures only. $CGX_SELL=0 disables it.
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
+  if (const char *env = std::getenv("CGX_SELL"))
+    if (std::atoi(env) == 0) return CGX_OK;
+  const int64_t n = A->dev.n, nnz = A->dev.nnz;
+  if (nnz < 1 || A->max_row_nnz > kSellMaxWidth) return CGX_OK;
+  cgx_ctx *ctx = A->ctx;
+  hipStream_t s = ctx->stream;
+  std::vector<int> hc;
+  if (!h_col) {
+    hc.resize((size_t)nnz);
+    CGX_HIP(hipMemcpyAsync(hc.data(), A->dev.col, (size_t)nnz * sizeof(int),
+                           hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    h_col = hc.data();
+  }
+  std::vector<SellSlice> sl;
+  std::vector<int> pool;
+  std::vector<unsigned long long> idx;
+  int64_t voff = 0;
+  if (!sell_plan_host(n, h_rowptr, h_col, sl, pool, idx, voff)) return CGX_OK;
+  const int64_t nsl = (int64_t)sl.size();
+  pool.resize(pool.size() + kSellMaxDict, 0);  // every lane of the last dictionary reads in bounds
+  const size_t es = dtype_size(A->dtype);
+  hipError_t e = hipMalloc(&A->d_sell_sl, sl.size() * sizeof(SellSlice));
+  if (e == hipSuccess) e = hipMalloc(&A->d_sell_dict, pool.size() * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&A->d_sell_idx, std::max<size_t>(idx.size(), 1) * 8);
+  if (e == hipSuccess)  // + one chunk of slack: the kernel reads 8 slots per chunk
+    e = hipMalloc(&A->d_sell_val, (size_t)(voff + 8 * kSellRows) * es);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(A->d_sell_sl, sl.data(), sl.size() * sizeof(SellSlice),
+                       hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(A->d_sell_dict, pool.data(), pool.size() * sizeof(int),
+                       hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !idx.empty())
+    e = hipMemcpyAsync(A->d_sell_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    free_sell(A);
+    return hip_fail(e, "cgx_csr_create(SELL copy)");
+  }
+  A->dev.sl = (const SellSlice *)A->d_sell_sl;
+  A->dev.sdict = (const int *)A->d_sell_dict;
+  A->dev.sidx = (const unsigned long long *)A->d_sell_idx;
+  A->dev.sval = A->d_sell_val;
+  A->dev.nsl = nsl;
+  A->dev.sell_maxw = 0;
+  for (const SellSlice &m : sl) A->dev.sell_maxw = std::max(A->dev.sell_maxw, m.width);
+  A->sell_padded = voff;
+  if (A->dtype == CGX_F32)
+    e = Launch<float>::sell_pack(A->dev, (const float *)A->dev.val, (float *)A->d_sell_val, s);
+  else
+    e = Launch<double>::sell_pack(A->dev, (const double *)A->dev.val, (double *)A->d_sell_val, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // host vectors die here
+  if (e != hipSuccess) {
+    free_sell(A);
+    return hip_fail(e, "cgx_csr_create(SELL pack)");
+  }
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  if (has_sell) *has_sell = A->dev.sl != nullptr;
+  if (padded) *padded = A->sell_padded;
+  return CGX_OK;
+}
+
+static bool known_variant(int v) {
+  static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
+                           68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
+                           267, 2048, 2050, 2056, 2058};
+  for (int k : ok)
+    if (k == v) return true;
+  return false;
+}
+
+extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  CGX_REQUIRE(known_variant(variant), CGX_EINVAL, "unknown SpMV variant %d", variant);
+  CGX_REQUIRE(!(variant & 2048) || A->dev.sl, CGX_EUNSUPPORTED,
+              "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
+  A->dev.variant = variant;
+  return CGX_OK;
+}
+
 // Pick the SpMV variant for this matrix on this device: the measured best
 // differs by matrix (non-temporal val/col loads help the 2-D 5-point matrix,
-// cost the 3-D 7-point one) and is cheap to measure — a few
-// launches on scratch vectors. $CGX_SPMV_VARIANT forces a variant.
+// cost the 3-D 7-point one; the SELL-64 copy, where the matrix has one,
+// streams 9 B per entry instead of 12) and is cheap to measure — a
+// few launches on scratch vectors. $CGX_SPMV_VARIANT forces a variant. The
+// SELL copy is freed when a CSR-stream variant wins.
 int autotune_spmv(cgx_csr *A) {
   if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
     A->dev.variant = std::atoi(env);
+    if (!(A->dev.variant & 2048)) free_sell(A);
     return CGX_OK;
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
-  if (bytes < (int64_t(64) << 20)) return CGX_OK;  // small: the size heuristic
-  static const int cands[] = {13, 15};
+  if (bytes < (int64_t(64) << 20)) {  // small: the size heuristic, SELL where built
+    if (A->dev.sl) A->dev.variant = 2048;
+    return CGX_OK;
+  }
+  // (the software-pipelined SELL forms, 2056/2058, measured slower than the
+  // plain ones on MI355X: profiles/r01_tune_sell.log; reachable by request)
+  std::vector<int> cands = {13, 15};
+  if (A->dev.sl) {
+    cands.push_back(2048);
+    cands.push_back(2050);
+  }
   cgx_ctx *ctx = A->ctx;
   hipStream_t s = ctx->stream;
   const size_t es = dtype_size(A->dtype);
@@ -539,35 +760,45 @@ int autotune_spmv(cgx_csr *A) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
-  float best = 1e30f;
-  int best_v = 0;
-  for (int v : cands) {
-    float tot = 0;
-    for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
-      if (rep == 1) e = hipEventRecord(e0, s);
-      if (e != hipSuccess) break;
-      if (A->dtype == CGX_F32)
-        e = Launch<float>::spmv_dot_variant(v, A->dev, (const float *)x, (float *)y,
-                                            (CgScalars<float> *)st, (RedWs<float> *)ctx->ws, s);
-      else
-        e = Launch<double>::spmv_dot_variant(v, A->dev, (const double *)x, (double *)y,
-                                             (CgScalars<double> *)st, (RedWs<double> *)ctx->ws,
-                                             s);
-    }
-    if (e == hipSuccess) e = hipEventRecord(e1, s);
-    if (e == hipSuccess) e = hipEventSynchronize(e1);
-    if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
-    if (e == hipSuccess && tot < best) {
-      best = tot;
-      best_v = v;
+  // interleaved rounds, best of each candidate: one round alone picks by
+  // the device's momentary state when candidates are within a few percent
+  std::vector<float> tbest(cands.size(), 1e30f);
+  for (int round = 0; round < 3 && e == hipSuccess; ++round) {
+    for (size_t ci = 0; ci < cands.size() && e == hipSuccess; ++ci) {
+      const int v = cands[ci];
+      float tot = 0;
+      for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
+        if (rep == 1) e = hipEventRecord(e0, s);
+        if (e != hipSuccess) break;
+        if (A->dtype == CGX_F32)
+          e = Launch<float>::spmv_dot_variant(v, A->dev, (const float *)x, (float *)y,
+                                              (CgScalars<float> *)st, (RedWs<float> *)ctx->ws,
+                                              s);
+        else
+          e = Launch<double>::spmv_dot_variant(v, A->dev, (const double *)x, (double *)y,
+                                               (CgScalars<double> *)st,
+                                               (RedWs<double> *)ctx->ws, s);
+      }
+      if (e == hipSuccess) e = hipEventRecord(e1, s);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
+      if (e == hipSuccess) tbest[ci] = std::min(tbest[ci], tot);
     }
   }
+  int best_v = 0;
+  float best = 1e30f;
+  for (size_t ci = 0; ci < cands.size(); ++ci)
+    if (tbest[ci] < best) {
+      best = tbest[ci];
+      best_v = cands[ci];
+    }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   for (void *p : {x, y, st})
     if (p) (void)hipFree(p);
   CGX_HIP(e);
   A->dev.variant = best_v;
+  if (!(best_v & 2048)) free_sell(A);
   return CGX_OK;
 }
 

@@ -88,17 +88,21 @@ __device__ __forceinline__ void block_sum(T (&v)[K], T *lds) {
 }
 
 // Grid-wide deterministic reduction. Every workgroup publishes its block sum
-// write-through and takes a ticket; the workgroup that takes the last ticket
-// sums all partials in workgroup order. Returns true in that workgroup, whose
-// thread 0 then holds the totals in v[].
+// write-through and takes the ticket of its group (blockIdx % kRedGroups). The
+// last arrival of a group sums the group's partials in workgroup order and
+// takes the top ticket; the last group sums the group sums in group order.
+// The result is independent of arrival order. Returns true in that final
+// workgroup, whose thread 0 then holds the totals in v[]. -DCGX_FLAT_TICKET
+// builds the single-ticket form (A/B only).
 template <typename T, int K>
 __device__ __forceinline__ bool grid_reduce(T (&v)[K], RedWs<T> *ws, T *lds, int *flag) {
   block_sum<T, K>(v, lds);
+#ifdef CGX_FLAT_TICKET
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k) store_sc1(&ws->partials[k * kMaxGrid + blockIdx.x], v[k]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED,
+    const unsigned prev = __hip_atomic_fetch_add(&ws->ticket[0], 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     *flag = (prev == gridDim.x - 1);
   }
@@ -115,9 +119,56 @@ __device__ __forceinline__ bool grid_reduce(T (&v)[K], RedWs<T> *ws, T *lds, int
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k) v[k] = acc[k];
-    __hip_atomic_store(&ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ws->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return true;
+#else
+  const unsigned G = gridDim.x;
+  const unsigned g = blockIdx.x % kRedGroups;
+  const unsigned ngroups = G < (unsigned)kRedGroups ? G : (unsigned)kRedGroups;
+  const unsigned members = (G - g + kRedGroups - 1) / kRedGroups;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) store_sc1(&ws->partials[k * kMaxGrid + blockIdx.x], v[k]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&ws->ticket[g], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (prev == members - 1);
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  // last of group g: sum the group's partials in workgroup order
+  T acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    acc[k] = T(0);
+    for (unsigned i = g + kRedGroups * threadIdx.x; i < G; i += kRedGroups * kBlock)
+      acc[k] += load_sc1(&ws->partials[k * kMaxGrid + i]);
+  }
+  block_sum<T, K>(acc, lds);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&ws->ticket[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < K; ++k) store_sc1(&ws->gsum[k * kRedGroups + g], acc[k]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&ws->top, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (prev == ngroups - 1);
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      T t = T(0);
+      for (unsigned q = 0; q < ngroups; ++q) t += load_sc1(&ws->gsum[k * kRedGroups + q]);
+      v[k] = t;
+    }
+    __hip_atomic_store(&ws->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+#endif
 }
 
 // XCD-grouped logical workgroup id: blocks b and b+8 share an XCD (observed
@@ -138,6 +189,12 @@ struct CsrArgs {
   const int *__restrict__ rbk;  // rowptr[rb[i]]: first entry of each row block
   int nrb;
   int64_t n;
+  // SELL-64 copy (variant bit 2048)
+  const SellSlice *__restrict__ sl;
+  const int *__restrict__ sdict;
+  const unsigned long long *__restrict__ sidx;
+  const void *sval;
+  int64_t nsl;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -169,6 +226,18 @@ template <typename T> struct PairOf;
 template <> struct PairOf<double> { typedef double V __attribute__((ext_vector_type(2))); };
 template <> struct PairOf<float> { typedef float V __attribute__((ext_vector_type(2))); };
 typedef int Int2 __attribute__((ext_vector_type(2)));
+
+// A paired (or quad) column load may run past the block's last entry kk1 - 1
+// and, in the matrix's last block, past the end of the column array: the
+// index it reads there is not a column. Elements at or past kk1 take the
+// first element's column (always in range); their products land in scratch
+// slots and are never summed. The over-read itself cannot fault: a pair
+// (quad) load is naturally aligned, so it never crosses a page the array's
+// last element does not also occupy.
+__device__ __forceinline__ Int2 tail_cols(Int2 c, int e0, int kk1) {
+  if (e0 + 1 >= kk1) c.y = c.x;
+  return c;
+}
 
 template <bool NT, typename P> __device__ __forceinline__ P ldg(const P *p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -236,7 +305,7 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
           for (int u = 0; u < U; ++u) {
             const int j = min(t + u * kBlock, npairs - 1);
             v[u] = ldg<NT>(v2 + j);
-            c[u] = ldg<NT>(c2 + j);
+            c[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, k0 + cnt);
           }
           T g0[U], g1[U];
 #pragma unroll
@@ -323,7 +392,7 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
     for (int u = 0; u < U; ++u) {
       const int j = min(t + u * kBlock, np - 1);
       vv[u] = ldg<NT>(v2 + j);
-      cc[u] = ldg<NT>(c2 + j);
+      cc[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, kk1);
     }
   };
   issue(k0, k1, v, c);
@@ -433,7 +502,10 @@ __device__ __forceinline__ void spmv_rows_deep(const CsrArgs &A, const T *__rest
     window(kk0, kk1, ka, np);
     const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
 #pragma unroll
-    for (int u = 0; u < U; ++u) cc[u] = ldg<NT>(c2 + min(t + u * kBlock, np - 1));
+    for (int u = 0; u < U; ++u) {
+      const int j = min(t + u * kBlock, np - 1);
+      cc[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, kk1);
+    }
   };
   auto load_v = [&](int kk0, int kk1, PV(&vv)[U]) {
     int ka, np;
@@ -559,7 +631,12 @@ __device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__rest
     for (int u = 0; u < U; ++u) {
       const int j = min(t + u * kBlock, nq - 1);
       vv[u] = ldg<NT>(v4 + j);
-      cc[u] = ldg<NT>(c4 + j);
+      Int4 q = ldg<NT>(c4 + j);
+      const int e0 = ka + 4 * j;  // see tail_cols
+      if (e0 + 1 >= kk1) q.y = q.x;
+      if (e0 + 2 >= kk1) q.z = q.x;
+      if (e0 + 3 >= kk1) q.w = q.x;
+      cc[u] = q;
     }
   };
   issue(k0, k1, v, c);
@@ -682,7 +759,7 @@ __device__ __forceinline__ void spmv_waves(const CsrArgs &A, const T *__restrict
     for (int u = 0; u < U; ++u) {
       const int j = min(lane + u * 64, np - 1);
       vv[u] = ldg<NT>(v2 + j);
-      cc[u] = ldg<NT>(c2 + j);
+      cc[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, kk1);
     }
   };
   issue(k0, k1, v, c);
@@ -748,16 +825,181 @@ __device__ __forceinline__ void spmv_waves(const CsrArgs &A, const T *__restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// SELL-64 SpMV (variant bit 2048; layout: cgx_internal.h SellSlice). One
+// wave per 64-row slice, lane l owns row 64 s + l and sums its entries in
+// ascending order in a register, so the row sums are bit-identical to the
+// CSR-stream forms (and to CG.hpp's SpMV) with no LDS staging and no rowptr
+// reads. A column is row + dict[k]: the slice's offset dictionary sits in
+// one VGPR (lane i holds entry i) and ds_bpermute fetches entry k, so the
+// index stream is 1 B per entry instead of 4 (9 B/entry in f64 instead of
+// 12). XCD split as variant bit 1: the waves of one XCD walk a contiguous
+// slice range, consecutive slices on the waves of one workgroup.
+// Bit 2: non-temporal value/index loads. Bit 16 (timing ablation, spmv_dot
+// only): no gathers.
+// ---------------------------------------------------------------------------
+template <typename T> struct SellLds {
+  T red[4 * kMaxRed];
+  int flag;
+  int rp[1];  // unused (keeps the SpmvLds member set)
+};
+
+// The waves of one XCD walk a contiguous slice range (as variant bit 1);
+// consecutive slices on the waves of one workgroup. Slice indices fit int
+// (n < 2^31), which keeps the loop control on the scalar unit.
+__device__ __forceinline__ void sell_range(int nsl, int &first, int &step, int &end) {
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = gridDim.x;
+  if ((G & 7) == 0) {
+    const int g = blockIdx.x & 7;
+    first = (int)(((int64_t)nsl * g) >> 3) + (blockIdx.x >> 3) * 4 + wid;
+    end = (int)(((int64_t)nsl * (g + 1)) >> 3);
+    step = (G >> 3) * 4;
+  } else {
+    first = blockIdx.x * 4 + wid;
+    end = nsl;
+    step = G * 4;
+  }
+}
+
+// One slice, any width. Every load is unconditional (no branches around
+// them, so the in-order vmcnt wait before the gathers covers the index word
+// only): slots past the slice width re-read the last slot (same lines: no
+// new L2 requests) and padding entries gather the row's own x (clamped to
+// the last row) and are dropped at the add.
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void sell_slice(const CsrArgs &A, const Gather &x, Epi &epi, int s) {
+  constexpr bool NT = (V & 2) != 0;
+  const T *__restrict__ sval = static_cast<const T *>(A.sval);
+  const int lane = threadIdx.x & 63;
+  const SellSlice m = A.sl[s];
+  const int row = s * kSellRows + lane;
+  const bool live = row < A.n;
+  const int rowc = live ? row : (int)A.n - 1;
+  epi.pre(rowc);
+  const int dv = A.sdict[m.dict + lane];
+  T acc = T(0);
+  for (int c = 0; c < m.width; c += 8) {
+    const unsigned long long iw =
+        ldg<NT>(A.sidx + m.ioff + (int64_t)(c >> 3) * kSellRows + lane);
+    const T *vp = sval + m.voff + (int64_t)c * kSellRows + lane;
+    T v[8], g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ldg<NT>(vp + min(j, m.width - 1 - c) * kSellRows);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned k = (unsigned)(iw >> (8 * j)) & 0xffu;
+      const int off = __builtin_amdgcn_ds_bpermute((int)(k << 2), dv);
+      if constexpr ((V & 16) != 0) g[j] = T(k & 1);
+      else g[j] = x(k != kSellPad ? row + off : rowc);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned k = (unsigned)(iw >> (8 * j)) & 0xffu;
+      const T t = acc + v[j] * g[j];
+      acc = (k != kSellPad) ? t : acc;
+    }
+  }
+  if (live) epi.row(row, acc);
+}
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sell(const CsrArgs &A, const Gather &x, Epi &epi) {
+  int s, step, end;
+  sell_range((int)A.nsl, s, step, end);
+  for (; s < end; s += step) sell_slice<T, V, Epi, Gather>(A, x, epi, s);
+}
+
+// Software-pipelined SELL (variant bits 2048 | 8; matrices whose slices are
+// at most 8 wide, one index word per row): while slice s gathers x and sums
+// its rows, the values, index word and dictionary of the wave's next slice
+// are in flight, so the HBM latency of the stream is off the slice's
+// critical path. Same sums, same order as spmv_sell. The loop runs over full
+// slices only (every lane a live row, so nothing is predicated and nothing
+// can be sunk past the prefetch); a partial last slice takes sell_slice.
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sell_pipe(const CsrArgs &A, const Gather &x, Epi &epi) {
+  constexpr bool NT = (V & 2) != 0;
+  const T *__restrict__ sval = static_cast<const T *>(A.sval);
+  const int lane = threadIdx.x & 63;
+  int first, step, end;
+  sell_range((int)A.nsl, first, step, end);
+  const int full = (int)(A.n / kSellRows);  // slices whose 64 rows all exist
+  const int pend = min(end, full);
+  auto issue = [&](int q, unsigned long long &iw, T(&v)[8], int &dv) {
+    // wave-uniform, read-only: a scalar load through the constant address
+    // space (a vector load would need a vmcnt(0) wait, draining the gathers
+    // in flight before the prefetch is issued)
+    const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
+    const int qi = __builtin_amdgcn_readfirstlane(q);
+    const int64_t voff = cs[qi].voff, ioff = cs[qi].ioff;
+    const int dict = cs[qi].dict, width = cs[qi].width;
+    const T *vp = sval + voff + lane;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ldg<NT>(vp + min(j, width - 1) * kSellRows);
+    iw = ldg<NT>(A.sidx + ioff + lane);
+    dv = A.sdict[dict + lane];
+  };
+  int s = first;
+  if (s < pend) {
+    unsigned long long iw;
+    T v[8];
+    int dv;
+    issue(s, iw, v, dv);
+    for (;;) {
+      const int ns = s + step;
+      const bool has_next = ns < pend;
+      const int row = s * kSellRows + lane;
+      epi.pre(row);
+      T g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned k = (unsigned)(iw >> (8 * j)) & 0xffu;
+        const int off = __builtin_amdgcn_ds_bpermute((int)(k << 2), dv);
+        if constexpr ((V & 16) != 0) g[j] = T(k & 1);
+        else g[j] = x(k != kSellPad ? row + off : row);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      unsigned long long iwn;
+      T vn[8];
+      int dvn;
+      issue(has_next ? ns : s, iwn, vn, dvn);
+      __builtin_amdgcn_sched_barrier(0);
+      T acc = T(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned k = (unsigned)(iw >> (8 * j)) & 0xffu;
+        const T t = acc + v[j] * g[j];
+        acc = (k != kSellPad) ? t : acc;
+      }
+      epi.row(row, acc);
+      if (!has_next) break;
+      iw = iwn;
+      dv = dvn;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = vn[j];
+      s = ns;
+    }
+    s += step;
+  }
+  // the partial last slice, if this wave owns it
+  for (; s < end; s += step)
+    if (s >= full) sell_slice<T, V, Epi, Gather>(A, x, epi, s);
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
-using LdsOf = typename std::conditional<(V & 512) != 0, WaveLds<T>,
-                                        SpmvLds<T, TileOf<V>::tile>>::type;
+using LdsOf = typename std::conditional<
+    (V & 2048) != 0, SellLds<T>,
+    typename std::conditional<(V & 512) != 0, WaveLds<T>, SpmvLds<T, TileOf<V>::tile>>::type>::type;
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
                                          const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
-  if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
+  if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
+  else if constexpr ((V & 2048) != 0) spmv_sell<T, V, Epi, Gather>(A, x, epi);
+  else if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 256) != 0) spmv_rows_quad<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 128) != 0) spmv_rows_deep<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 8) != 0) spmv_rows_pipe<T, V, Epi, Gather>(A, val, x, epi, sm);
@@ -1143,6 +1385,26 @@ __global__ __launch_bounds__(kBlock) void k_gather(const T *__restrict__ src,
     dst[i] = src[idx[i]];
 }
 
+// SELL-64 values: slot j of row i = val[rowptr[i] + j], 0 past the row's end
+// (those slots carry the padding index, the SpMV never multiplies them).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sell_pack(int64_t n, int64_t nsl,
+                                                      const int *__restrict__ rowptr,
+                                                      const T *__restrict__ val,
+                                                      const SellSlice *__restrict__ sl,
+                                                      T *__restrict__ sval) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nsl * kSellRows;
+       i += stride) {
+    const SellSlice m = sl[i / kSellRows];
+    const int l = (int)(i % kSellRows);
+    const int a = i < n ? rowptr[i] : 0;
+    const int len = i < n ? rowptr[i + 1] - a : 0;
+    for (int j = 0; j < m.width; ++j)
+      sval[m.voff + (int64_t)j * kSellRows + l] = j < len ? val[a + j] : T(0);
+  }
+}
+
 // Poisson rows [row_begin, row_end): columns ascending (-z,-y,-x,d,+x,+y,+z).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_poisson(int dim, int nx, int ny, int nz,
@@ -1181,7 +1443,9 @@ inline int elem_grid(int64_t n, int per_thread) {
   return (int)g;
 }
 
-inline CsrArgs args(const CsrDev &A) { return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb, A.n}; }
+inline CsrArgs args(const CsrDev &A) {
+  return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb, A.n, A.sl, A.sdict, A.sidx, A.sval, A.nsl};
+}
 
 }  // namespace
 
@@ -1223,6 +1487,11 @@ constexpr int64_t kNtMinBytes = int64_t(256) << 20;
 
 template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   if (v < 0 && A.variant > 0) v = A.variant;  // chosen by cgx_csr_create's autotune
+  if (v >= 0 && (v & 2048)) {
+    // pipelined SELL (bit 8) needs slices of at most 8 entries per row
+    if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
+    v = -1;  // no SELL copy: CSR-stream
+  }
   if (v < 0) v = (A.nnz * int64_t(sizeof(T) + sizeof(int)) >= kNtMinBytes) ? 15 : 13;
   v &= 1023;  // bits 16/32: timing ablations, only reachable through cgx_tune_spmv
   const int tile = A.tile == 1024 ? 64 : 0;  // the kernel tile follows the schedule
@@ -1285,6 +1554,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 77: CGX_LAUNCH_V(KERNEL, 77, __VA_ARGS__);                                    \
     case 78: CGX_LAUNCH_V(KERNEL, 78, __VA_ARGS__);                                    \
     case 79: CGX_LAUNCH_V(KERNEL, 79, __VA_ARGS__);                                    \
+    case 2048: CGX_LAUNCH_V(KERNEL, 2048, __VA_ARGS__);                               \
+    case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);                               \
+    case 2056: CGX_LAUNCH_V(KERNEL, 2056, __VA_ARGS__);                               \
+    case 2058: CGX_LAUNCH_V(KERNEL, 2058, __VA_ARGS__);                               \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -1313,6 +1586,10 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 63: CGX_LAUNCH_V(k_spmv_dot, 63, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 2064: CGX_LAUNCH_V(k_spmv_dot, 2064, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 2066: CGX_LAUNCH_V(k_spmv_dot, 2066, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 2072: CGX_LAUNCH_V(k_spmv_dot, 2072, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 2074: CGX_LAUNCH_V(k_spmv_dot, 2074, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -1383,6 +1660,12 @@ template <typename T>
 hipError_t Launch<T>::gather(const T *src, const int *idx, int64_t n, T *dst,
                              hipStream_t s) {
   CGX_LAUNCH(k_gather<T>, elem_grid(n, 4), src, idx, n, dst);
+}
+
+template <typename T>
+hipError_t Launch<T>::sell_pack(const CsrDev &A, const T *val, T *sval, hipStream_t s) {
+  CGX_LAUNCH(k_sell_pack<T>, elem_grid(A.nsl * kSellRows, 4), A.n, A.nsl, A.rowptr, val, A.sl,
+             sval);
 }
 
 template struct Launch<double>;

@@ -83,6 +83,10 @@ struct cgx_csr {
   int64_t n_global = 0, row_begin = 0;
   cgx::Halo halo;
   void *d_ext = nullptr;  // scratch vector with ghost area (n + n_ghost)
+  // SELL-64 copy (cgx::CsrDev::sl ...), null when absent
+  void *d_sell_sl = nullptr, *d_sell_dict = nullptr, *d_sell_idx = nullptr;
+  void *d_sell_val = nullptr;
+  int64_t sell_padded = 0;
 };
 
 struct cgx_cg {

@@ -78,6 +78,14 @@ int cgx_csr_set_tile(cgx_csr *csr, int tile);
 /* SpMV variant cgx_csr_create picked for this matrix by timing the candidate
  * kernels on the device ($CGX_SPMV_VARIANT overrides; 0 = size heuristic). */
 int cgx_csr_variant(cgx_csr *csr, int *variant);
+/* Force the SpMV variant of this matrix (0: size heuristic). Variants with
+ * bit 2048 use the SELL-64 copy cgx_csr_create builds for matrices whose
+ * slices of 64 rows have at most 64 distinct (col - row) offsets; they fail
+ * with CGX_EUNSUPPORTED when the matrix has none (or it was freed because
+ * the autotune chose a CSR-stream variant). */
+int cgx_csr_set_variant(cgx_csr *csr, int variant);
+/* 1 if the matrix holds a SELL-64 copy, else 0; its padded entry count. */
+int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
  * Scalars are DEVICE pointers, as in the reference (Scalar<DT>::ptr()). */
@@ -196,6 +204,15 @@ int cgx_plan_remap(int64_t n_local, int64_t row_begin, int64_t nnz, int *col,
 int cgx_row_blocks(const int *h_rowptr, int64_t n, int64_t *nrb, int **rb,
                    int *max_row_nnz);
 void cgx_free_host(void *p);
+/* Host-only: the SELL-64 layout cgx_csr_create would build for a host CSR
+ * (DESIGN.md §SpMV formats). *nsl = 0 when the matrix does not qualify.
+ * slices[4 q .. 4 q + 3] = {first value slot, first index word, first
+ * dictionary entry, width} of slice q; dict[ndict] = the offset pool (col -
+ * row), idx[nidx] = 8 one-byte dictionary indices per word (0xff: padding);
+ * value_slots = length of the value array. Release with cgx_free_host. */
+int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+                  int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,
+                  unsigned long long **idx, int64_t *value_slots);
 
 /* ---- diagnostics ------------------------------------------------------------
  * Average device time (ms) of `iters` launches of the SpMV + p.Ap kernel in

@@ -1,0 +1,140 @@
+"""SELL-64 layout (cgx_sell_plan, host-only) checked on the CPU.
+
+The test emulates spmv_sell's addressing (cgx_kernels.hip) lane by lane in
+numpy. Every index the kernel forms must fall inside the arrays
+cgx_csr_create allocates:
+  * values: value_slots + 8 * 64, for the chunk of slack;
+  * index words: nidx;
+  * dictionary pool: ndict;
+  * gathered x: n.
+With values packed the way k_sell_pack packs them, the emulated row sums
+must equal the oracle's SpMV bit for bit.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conjugategradient_amd._native import check, lib
+from tests.util import irregular_spd
+
+ROWS = 64
+PAD = 0xFF
+
+
+def sell_plan(rp, cl):
+    L = lib()
+    nsl, ndict, nidx, slots = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+    sl = C.POINTER(C.c_int64)()
+    dic = C.POINTER(C.c_int32)()
+    idx = C.POINTER(C.c_uint64)()
+    rp = np.ascontiguousarray(rp, np.int32)
+    cl = np.ascontiguousarray(cl, np.int32)
+    check(L.cgx_sell_plan(rp.ctypes.data, cl.ctypes.data, len(rp) - 1, C.byref(nsl), C.byref(sl),
+                          C.byref(ndict), C.byref(dic), C.byref(nidx), C.byref(idx),
+                          C.byref(slots)))
+    if nsl.value == 0:
+        return None
+    out = (np.ctypeslib.as_array(sl, shape=(nsl.value, 4)).copy(),
+           np.ctypeslib.as_array(dic, shape=(ndict.value,)).copy(),
+           np.ctypeslib.as_array(idx, shape=(max(nidx.value, 1),))[:nidx.value].copy(),
+           slots.value)
+    for p in (sl, dic, idx):
+        L.cgx_free_host(C.cast(p, C.c_void_p))
+    return out
+
+
+def pack_values(rp, vl, sl, slots):
+    """k_sell_pack: slot j of row i = val[rowptr[i] + j], 0 past the row."""
+    n = len(rp) - 1
+    sval = np.zeros(slots + 8 * ROWS, vl.dtype)
+    for q, (voff, _, _, w) in enumerate(sl):
+        for l in range(ROWS):
+            i = q * ROWS + l
+            if i >= n:
+                continue
+            a, e = rp[i], rp[i + 1]
+            for j in range(e - a):
+                sval[voff + j * ROWS + l] = vl[a + j]
+    return sval
+
+
+def emulate_spmv(rp, sl, dic, idx, sval, x):
+    """spmv_sell, with every index the kernel forms checked against the
+    array extents cgx_csr_create allocates."""
+    n = len(rp) - 1
+    y = np.zeros(n)
+    lane = np.arange(ROWS)
+    for q, (voff, ioff, dbase, w) in enumerate(sl):
+        row = q * ROWS + lane
+        live = row < n
+        rowc = np.where(live, row, n - 1)
+        assert dbase + ROWS <= len(dic)
+        dv = dic[dbase + lane]
+        acc = np.zeros(ROWS)
+        for c in range(0, w, 8):
+            wi = ioff + (c >> 3) * ROWS + lane
+            assert wi.max() < len(idx)
+            iw = idx[wi]
+            for j in range(8):
+                vi = voff + (c + j) * ROWS + lane
+                assert vi.max() < len(sval)
+                v = sval[vi]
+                k = ((iw >> np.uint64(8 * j)) & np.uint64(0xFF)).astype(np.int64)
+                off = dv[(k * 4 // 4) % ROWS]              # ds_bpermute
+                g_idx = np.where(k != PAD, row + off, rowc)
+                assert g_idx.min() >= 0 and g_idx.max() < n
+                g = x[g_idx]
+                with np.errstate(invalid="ignore"):
+                    t = acc + v * g
+                acc = np.where(k != PAD, t, acc)
+        y[row[live]] = acc[live]
+    return y
+
+
+def cases(oracle):
+    from tests.test_gpu_sell import banded
+    return {
+        "poisson3d_ragged": oracle.poisson(3, 23, 19, 17),
+        "poisson2d": oracle.poisson(2, 40, 33, 1),
+        "banded": banded(5_003, half=9),
+        "empty_rows": banded(2_001, half=6, empty_every=13),
+        "tiny": (np.array([0, 1, 3, 4], np.int32), np.array([0, 0, 1, 2], np.int32),
+                 np.array([2.0, -1.0, 3.0, 4.0])),
+        "wide": banded(777, half=25),   # rows > 8 entries: several index words
+    }
+
+
+@pytest.mark.parametrize("case", ["poisson3d_ragged", "poisson2d", "banded", "empty_rows",
+                                  "tiny", "wide"])
+def test_sell_layout_in_bounds_and_bitexact(oracle, case):
+    rp, cl, vl = cases(oracle)[case]
+    plan = sell_plan(rp, cl)
+    assert plan is not None, case
+    sl, dic, idx, slots = plan
+    n = len(rp) - 1
+    assert len(sl) == (n + ROWS - 1) // ROWS
+    assert (sl[:, 3] <= 64).all() and slots == (sl[:, 3] * ROWS).sum()
+    # dictionary indices < 64, every real entry present exactly once
+    b = idx.view(np.uint8)
+    assert ((b == PAD) | (b < 64)).all()
+    assert (b != PAD).sum() == len(vl)
+    sval = pack_values(rp, vl, sl, slots)
+    x = np.random.default_rng(1).standard_normal(n)
+    np.testing.assert_array_equal(emulate_spmv(rp, sl, dic, idx, sval, x),
+                                  oracle.spmv(rp, cl, vl, x))
+
+
+def test_sell_dictionaries_are_shared(oracle):
+    rp, cl, _ = oracle.poisson(3, 32, 32, 32)
+    sl, dic, _, _ = sell_plan(rp, cl)
+    # interior slices of a stencil share a handful of dictionaries
+    assert len(np.unique(sl[:, 2])) < 40
+    assert len(dic) < 40 * 7 + 64
+
+
+def test_sell_rejects_scattered_and_long_rows():
+    rp, cl, _ = irregular_spd(20_000, seed=4)
+    assert sell_plan(rp, cl) is None
+    rp, cl, _ = irregular_spd(5_000, seed=5, hub=3000)   # one row of ~3000 entries
+    assert sell_plan(rp, cl) is None

@@ -47,6 +47,8 @@ def main():
     L = lib()
     q = cga.Queue(0)
     variants = [int(v) for v in a.variants.split(",")]
+    if any(v & 2048 for v in variants):  # keep the SELL-64 copy (autotune may free it)
+        os.environ.setdefault("CGX_SPMV_VARIANT", "2048")
     for name in a.configs.split(","):
         A = matrix(q, name)
         n, nnz = A.N(), A.NNZ()
