@@ -5,11 +5,14 @@ behind the interfaces of XeniaHerr/ConjugateGradient:
 
 * C++: include/CG.hpp, include/VectorOperations.hpp,
   include/LinearAlgebraTypes.hpp (drop-in for src/*.hpp);
-* Python: the same classes in ``conjugategradient_amd.core``.
+* Python: the same classes in ``conjugategradient_amd.core``; the
+  Matrix-Market loader (test/mm_reader.cpp read_file) in ``.mtx``.
 """
 from ._native import CgxError, device_count, header_symbols, lib  # noqa: F401
 from .core import (CG, DeviceArray, Debuglevel, Event, Matrix, Queue, Scalar,  # noqa: F401
                    Vector, VectorOperations)
+from .mtx import read_file, write_mtx_lower  # noqa: F401
 
 __all__ = ["CG", "CgxError", "Debuglevel", "DeviceArray", "Event", "Matrix", "Queue", "Scalar",
-           "Vector", "VectorOperations", "device_count", "header_symbols", "lib"]
+           "Vector", "VectorOperations", "device_count", "header_symbols", "lib", "read_file",
+           "write_mtx_lower"]

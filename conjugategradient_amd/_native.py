@@ -61,6 +61,7 @@ _SIGS = {
     "cgx_csr_set_tile": (_i32, [_vp, _i32]),
     "cgx_csr_variant": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_set_variant": (_i32, [_vp, _i32]),
+    "cgx_csr_set_sell": (_i32, [_vp, _i32]),
     "cgx_csr_sell_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(C.c_int64)]),
     "cgx_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
                             C.POINTER(_i32)]),
@@ -97,7 +98,11 @@ _SIGS = {
                                C.POINTER(C.POINTER(_i64)), _vp]),
     "cgx_plan_remap": (_i32, [_i64, _i64, _i64, _vp, _i64, _vp]),
     "cgx_free_host": (None, [_vp]),
-    "cgx_sell_plan": (_i32, [_vp, _vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
+    "cgx_mm_read": (_i32, [C.c_char_p, _i32, C.POINTER(_i64), C.POINTER(_i64),
+                           C.POINTER(C.POINTER(_i32)), C.POINTER(C.POINTER(_i32)),
+                           C.POINTER(C.POINTER(C.c_double))]),
+    "cgx_mm_write_lower": (_i32, [C.c_char_p, _i64, _vp, _vp, _vp, _i32]),
+    "cgx_sell_plan": (_i32, [_vp, _vp, _i64, _i32, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
                              C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
                              C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(_i64)]),
     "cgx_tune_spmv": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, C.POINTER(_dbl)]),

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cgx_objects.h"
@@ -300,6 +301,10 @@ extern "C" int cgx_destroy(cgx_ctx *ctx) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  for (int b = 0; b < 2; ++b) {
+    if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
+    if (ctx->stage_ev[b]) (void)hipEventDestroy(ctx->stage_ev[b]);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return CGX_OK;
@@ -349,6 +354,46 @@ extern "C" int cgx_free(cgx_ctx *ctx, void *d) {
   return CGX_OK;
 }
 
+// Large device -> host copies into pageable memory (extract() of a 256^3
+// solution, a CSR download) go through a ring of two pinned 64 MiB chunks:
+// the DMA engine fills chunk k+1 while several host threads copy chunk k out
+// (15-17 GB/s against 10 for one hipMemcpy, profiles/r01_setup.json). Small
+// copies, and $CGX_STAGED=0, use one hipMemcpyAsync.
+constexpr size_t kStageChunk = size_t(64) << 20;
+constexpr size_t kStageMin = size_t(16) << 20;
+
+static bool staged(size_t bytes) {
+  if (bytes < kStageMin) return false;
+  const char *e = std::getenv("CGX_STAGED");
+  return !(e && std::atoi(e) == 0);
+}
+
+static int ensure_stage(cgx_ctx *ctx) {
+  for (int b = 0; b < 2; ++b) {
+    if (!ctx->stage[b]) CGX_HIP(hipHostMalloc(&ctx->stage[b], kStageChunk, hipHostMallocDefault));
+    if (!ctx->stage_ev[b]) CGX_HIP(hipEventCreateWithFlags(&ctx->stage_ev[b], hipEventDisableTiming));
+  }
+  return CGX_OK;
+}
+
+static void par_memcpy(void *dst, const void *src, size_t len) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::min(hw ? hw : 1u, 8u), len >> 22));
+  if (nt <= 1) {
+    std::memcpy(dst, src, len);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const size_t a = len * t / nt, b = len * (t + 1) / nt;
+    th.emplace_back([=] { std::memcpy((char *)dst + a, (const char *)src + a, b - a); });
+  }
+  for (auto &x : th) x.join();
+}
+
+// Host -> device: ROCm's pageable path already runs at 50-55 GB/s for a
+// 1.5 GB CSR on MI355X (a pinned ring measured no faster:
+// profiles/r01_setup.json), so one hipMemcpyAsync.
 extern "C" int cgx_h2d(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
   CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
   DeviceGuard g(ctx->device);
@@ -367,8 +412,31 @@ extern "C" int cgx_h2d_async(cgx_ctx *ctx, void *dst, const void *src, size_t by
 extern "C" int cgx_d2h(cgx_ctx *ctx, void *dst, const void *src, size_t bytes) {
   CGX_REQUIRE(ctx && (bytes == 0 || (dst && src)), CGX_EINVAL, "NULL argument");
   DeviceGuard g(ctx->device);
-  CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  CGX_HIP(hipStreamSynchronize(ctx->stream));
+  if (!staged(bytes)) {
+    CGX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    CGX_HIP(hipStreamSynchronize(ctx->stream));
+    return CGX_OK;
+  }
+  if (int rc = ensure_stage(ctx)) return rc;
+  // DMA chunk k+1 while the host copies chunk k out of the ring
+  const size_t nchunks = (bytes + kStageChunk - 1) / kStageChunk;
+  auto issue = [&](size_t k) -> int {
+    const int b = (int)(k & 1);
+    const size_t off = k * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    CGX_HIP(hipMemcpyAsync(ctx->stage[b], (const char *)src + off, len, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    CGX_HIP(hipEventRecord(ctx->stage_ev[b], ctx->stream));
+    return CGX_OK;
+  };
+  if (int rc = issue(0)) return rc;
+  for (size_t k = 0; k < nchunks; ++k) {
+    if (k + 1 < nchunks)
+      if (int rc = issue(k + 1)) return rc;
+    const int b = (int)(k & 1);
+    const size_t off = k * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    CGX_HIP(hipEventSynchronize(ctx->stage_ev[b]));
+    par_memcpy((char *)dst + off, ctx->stage[b], len);
+  }
   return CGX_OK;
 }
 
@@ -389,7 +457,7 @@ extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
 }
 
 int autotune_spmv(cgx_csr *A);
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col);
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
 void free_sell(cgx_csr *A);
 
 // ===========================================================================
@@ -446,7 +514,7 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   A->dev.rb = A->d_rb;
   A->dev.rbk = A->d_rb + nrb1;
   A->n_global = n;
-  int rc = build_sell(A, h_rowptr, nullptr);
+  int rc = build_sell(A, h_rowptr, nullptr, 0);
   if (!rc) rc = autotune_spmv(A);
   if (rc) {
     cgx_csr_destroy(A);
@@ -501,7 +569,7 @@ extern "C" int cgx_csr_set_tile(cgx_csr *A, int tile) {
 
 extern "C" int cgx_csr_variant(cgx_csr *A, int *variant) {
   CGX_REQUIRE(A && variant, CGX_EINVAL, "NULL argument");
-  *variant = A->dev.variant;
+  *variant = launch_variant(A->dev, A->dtype);
   return CGX_OK;
 }
 
@@ -524,32 +592,35 @@ void free_sell(cgx_csr *A) {
   A->dev.sidx = nullptr;
   A->dev.sval = nullptr;
   A->dev.nsl = 0;
+  A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
   A->sell_padded = 0;
 }
 
-// SELL-64 layout of a host CSR (cgx_internal.h SellSlice; DESIGN.md §SpMV
-// formats). Qualifies when every 64-row slice has rows of at most
-// kSellMaxWidth entries and at most kSellMaxDict distinct (col - row)
-// offsets, and the padding adds at most a quarter of the entries (+4096) — stencil
-// and other banded matrices. Returns false (outputs unspecified) otherwise.
-// voff_total: value slots of the layout (the kernel reads one chunk beyond).
-static bool sell_plan_host(int64_t n, const int *rowptr, const int *col,
+// SELL layout of a host CSR (cgx_internal.h SellSlice; DESIGN.md §SpMV
+// formats) with R rows per lane (slices of 64 R rows). Qualifies when every
+// slice has rows of at most kSellMaxWidth entries and at most kSellMaxDict
+// distinct (col - row) offsets, and the padding adds at most a quarter of the
+// entries (+4096) — stencil and other banded matrices. Returns false
+// (outputs unspecified) otherwise. voff_total: value slots of the layout
+// (the kernel reads one chunk beyond).
+static bool sell_plan_host(int64_t n, const int *rowptr, const int *col, int R,
                            std::vector<SellSlice> &sl, std::vector<int> &pool,
                            std::vector<unsigned long long> &idx, int64_t &voff_total) {
   const int64_t nnz = (int64_t)rowptr[n] - rowptr[0];
-  if (nnz < 1 || n + kSellRows >= (int64_t(1) << 31)) return false;
-  const int64_t nsl = (n + kSellRows - 1) / kSellRows;
+  const int64_t H = (int64_t)kSellRows * R;  // rows per slice
+  if (nnz < 1 || (R != 1 && R != 2) || n + H >= (int64_t(1) << 31)) return false;
+  const int64_t nsl = (n + H - 1) / H;
   sl.assign((size_t)nsl, SellSlice{});
   int64_t voff = 0, ioff = 0, padded = 0;
   for (int64_t q = 0; q < nsl; ++q) {
-    const int64_t r0 = q * kSellRows, r1 = std::min(n, r0 + kSellRows);
+    const int64_t r0 = q * H, r1 = std::min(n, r0 + H);
     int w = 0;
     for (int64_t i = r0; i < r1; ++i) w = std::max(w, rowptr[i + 1] - rowptr[i]);
     if (w > kSellMaxWidth) return false;
     sl[(size_t)q] = SellSlice{voff, ioff, 0, w};
-    voff += (int64_t)kSellRows * w;
-    ioff += (int64_t)kSellRows * ((w + 7) / 8);
+    voff += H * w;
+    ioff += H * ((w + 7) / 8);
     padded += (r1 - r0) * w;
   }
   if (padded > nnz + nnz / 4 + 4096) return false;  // small matrices: padding is noise
@@ -561,9 +632,10 @@ static bool sell_plan_host(int64_t n, const int *rowptr, const int *col,
   d.reserve(kSellMaxDict);
   for (int64_t q = 0; q < nsl; ++q) {
     SellSlice &m = sl[(size_t)q];
-    const int64_t r0 = q * kSellRows, r1 = std::min(n, r0 + kSellRows);
+    const int64_t r0 = q * H, r1 = std::min(n, r0 + H);
     d.clear();
     for (int64_t i = r0; i < r1; ++i) {
+      const int64_t l = (i - r0) / R, r = (i - r0) % R;  // lane, row of the lane
       for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
         const int off = col[k] - (int)i;
         size_t t = 0;
@@ -573,7 +645,8 @@ static bool sell_plan_host(int64_t n, const int *rowptr, const int *col,
           d.push_back(off);
         }
         const int j = k - rowptr[i];
-        unsigned long long &wd = idx[(size_t)(m.ioff + (int64_t)(j >> 3) * kSellRows + (i - r0))];
+        unsigned long long &wd =
+            idx[(size_t)(m.ioff + ((int64_t)(j >> 3) * kSellRows + l) * R + r)];
         const int sh = 8 * (j & 7);
         wd = (wd & ~(0xffull << sh)) | ((unsigned long long)t << sh);
       }
@@ -597,7 +670,8 @@ static bool sell_plan_host(int64_t n, const int *rowptr, const int *col,
   return true;
 }
 
-extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int rows_per_lane,
+                             int64_t *nsl,
                              int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,
                              unsigned long long **idx, int64_t *value_slots) {
   CGX_REQUIRE(h_rowptr && h_col && nsl && slices && ndict && dict && nidx && idx && value_slots,
@@ -611,7 +685,8 @@ extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, i
   *slices = nullptr;
   *dict = nullptr;
   *idx = nullptr;
-  if (!sell_plan_host(n, h_rowptr, h_col, sl, pool, ix, voff)) return CGX_OK;
+  CGX_REQUIRE(rows_per_lane == 1 || rows_per_lane == 2, CGX_EINVAL, "rows_per_lane must be 1 or 2");
+  if (!sell_plan_host(n, h_rowptr, h_col, rows_per_lane, sl, pool, ix, voff)) return CGX_OK;
   *slices = (int64_t *)std::malloc(std::max<size_t>(sl.size(), 1) * 4 * sizeof(int64_t));
   *dict = (int *)std::malloc(pool.size() * sizeof(int));
   *idx = (unsigned long long *)std::malloc(std::max<size_t>(ix.size(), 1) * 8);
@@ -631,17 +706,32 @@ extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, i
   return CGX_OK;
 }
 
-// SELL-64 copy of A on the device, when the matrix qualifies (sell_plan_host);
-// otherwise A keeps only the CSR-stream schedule and this returns CGX_OK.
-// Errors are device failures only. $CGX_SELL=0 disables it.
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
-  if (const char *env = std::getenv("CGX_SELL"))
-    if (std::atoi(env) == 0) return CGX_OK;
+// SELL copy of A on the device with R rows per lane (0: the default layout),
+// when the matrix qualifies (sell_plan_host); otherwise A keeps only the
+// CSR-stream schedule and this returns CGX_OK. Errors are device failures
+// only. $CGX_SELL=0 disables it, =1 / =2 selects R.
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
+  if (R == 0) {
+    R = kSellDefaultR;
+    if (const char *env = std::getenv("CGX_SELL")) {
+      R = std::atoi(env);
+      if (R == 0) return CGX_OK;
+      if (R != 1 && R != 2) R = kSellDefaultR;
+    }
+  }
+  free_sell(A);
   const int64_t n = A->dev.n, nnz = A->dev.nnz;
   if (nnz < 1 || A->max_row_nnz > kSellMaxWidth) return CGX_OK;
   cgx_ctx *ctx = A->ctx;
   hipStream_t s = ctx->stream;
-  std::vector<int> hc;
+  std::vector<int> hc, hr;
+  if (!h_rowptr) {
+    hr.resize((size_t)n + 1);
+    CGX_HIP(hipMemcpyAsync(hr.data(), A->dev.rowptr, hr.size() * sizeof(int),
+                           hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    h_rowptr = hr.data();
+  }
   if (!h_col) {
     hc.resize((size_t)nnz);
     CGX_HIP(hipMemcpyAsync(hc.data(), A->dev.col, (size_t)nnz * sizeof(int),
@@ -653,7 +743,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
   std::vector<int> pool;
   std::vector<unsigned long long> idx;
   int64_t voff = 0;
-  if (!sell_plan_host(n, h_rowptr, h_col, sl, pool, idx, voff)) return CGX_OK;
+  if (!sell_plan_host(n, h_rowptr, h_col, R, sl, pool, idx, voff)) return CGX_OK;
   const int64_t nsl = (int64_t)sl.size();
   pool.resize(pool.size() + kSellMaxDict, 0);  // every lane of the last dictionary reads in bounds
   const size_t es = dtype_size(A->dtype);
@@ -661,7 +751,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
   if (e == hipSuccess) e = hipMalloc(&A->d_sell_dict, pool.size() * sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&A->d_sell_idx, std::max<size_t>(idx.size(), 1) * 8);
   if (e == hipSuccess)  // + one chunk of slack: the kernel reads 8 slots per chunk
-    e = hipMalloc(&A->d_sell_val, (size_t)(voff + 8 * kSellRows) * es);
+    e = hipMalloc(&A->d_sell_val, (size_t)(voff + 8 * kSellRows * R) * es);
   if (e == hipSuccess)
     e = hipMemcpyAsync(A->d_sell_sl, sl.data(), sl.size() * sizeof(SellSlice),
                        hipMemcpyHostToDevice, s);
@@ -679,6 +769,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
   A->dev.sidx = (const unsigned long long *)A->d_sell_idx;
   A->dev.sval = A->d_sell_val;
   A->dev.nsl = nsl;
+  A->dev.sell_r = R;
   A->dev.sell_maxw = 0;
   for (const SellSlice &m : sl) A->dev.sell_maxw = std::max(A->dev.sell_maxw, m.width);
   A->sell_padded = voff;
@@ -694,9 +785,25 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col) {
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_set_sell(cgx_csr *A, int rows_per_lane) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  CGX_REQUIRE(rows_per_lane >= 0 && rows_per_lane <= 2, CGX_EINVAL,
+              "rows_per_lane must be 0 (drop the SELL copy), 1 or 2");
+  DeviceGuard g(A->ctx->device);
+  if (rows_per_lane == 0) {
+    free_sell(A);
+    if (A->dev.variant & 2048) A->dev.variant = 0;
+    return CGX_OK;
+  }
+  int rc = build_sell(A, nullptr, nullptr, rows_per_lane);
+  if (rc) return rc;
+  if (!A->dev.sl && (A->dev.variant & 2048)) A->dev.variant = 0;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
-  if (has_sell) *has_sell = A->dev.sl != nullptr;
+  if (has_sell) *has_sell = A->dev.sl ? A->dev.sell_r : 0;
   if (padded) *padded = A->sell_padded;
   return CGX_OK;
 }
@@ -704,7 +811,7 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
 static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
                            68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
-                           267, 2048, 2050, 2056, 2058};
+                           267, 2048, 2050, 2056, 2058, 6144, 6146};
   for (int k : ok)
     if (k == v) return true;
   return false;

@@ -27,7 +27,7 @@
 #include "cgx_objects.h"
 
 int autotune_spmv(cgx_csr *A);  // cgx_abi.cpp
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col);
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
 
 namespace cgx {
 
@@ -475,7 +475,7 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   A->max_row_nnz = mx;
   A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, A->d_rb + nrb1,
                   (int)nrb1 - 1, kTile};
-  if ((rc = build_sell(A, hrp.data(), hcol.data())) || (rc = autotune_spmv(A))) {
+  if ((rc = build_sell(A, hrp.data(), hcol.data(), 0)) || (rc = autotune_spmv(A))) {
     cgx_csr_destroy(A);
     return rc;
   }

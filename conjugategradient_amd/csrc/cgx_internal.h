@@ -53,15 +53,19 @@ template <typename T> struct RedWs {
   T partials[kMaxRed * kMaxGrid];
 };
 
-// SELL-64 copy of a matrix (built by cgx_csr_create when the matrix
-// qualifies, DESIGN.md §SpMV formats): rows in slices of 64, one wave per
-// slice, lane l owns row 64 s + l. Entry j of that row sits at
-// val[voff + 64 j + l]; its column is row + dict[dict + k] where k is byte
-// j % 8 of the 64-bit word idx[ioff + 64 (j / 8) + l] (k = 0xff: padding).
+// SELL copy of a matrix (built by cgx_csr_create when the matrix qualifies,
+// DESIGN.md §SpMV formats), R = 1 or 2 rows per lane: rows in slices of
+// 64 R, one wave per slice, lane l owns rows 64 R s + R l + r (r < R).
+// Entry j of that row sits at val[voff + (64 j + l) R + r]; its column is
+// row + dict[dict + k] where k is byte j % 8 of the 64-bit word
+// idx[ioff + (64 (j / 8) + l) R + r] (k = 0xff: padding). R = 2 makes every
+// value and index access of a lane one 16-byte load.
 constexpr int kSellRows = 64;
 constexpr int kSellMaxDict = 64;    // distinct (col - row) per slice: one VGPR
 constexpr int kSellMaxWidth = 64;   // longest row of a slice
 constexpr unsigned kSellPad = 0xff;
+constexpr int kSellDefaultR = 2;    // rows per lane of the SELL copy cgx_csr_create builds
+                                    // (2: 16-byte loads, profiles/r01_tune_sell2.log)
 struct SellSlice {
   int64_t voff;  // first value of the slice (entries)
   int64_t ioff;  // first index word of the slice
@@ -87,6 +91,7 @@ struct CsrDev {
   const void *sval = nullptr;
   int64_t nsl = 0;
   int sell_maxw = 0;  // widest slice
+  int sell_r = 1;     // rows per lane of the SELL copy
 };
 
 template <typename T> struct Launch {
@@ -127,6 +132,9 @@ template <typename T> struct Launch {
 
 // axpby modes
 enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
+
+// the SpMV variant a launch on A uses (dtype: CGX_F64 / CGX_F32)
+int launch_variant(const CsrDev &A, int dtype);
 
 // host-side row-block schedule (cgx_abi.cpp)
 std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz,

@@ -987,6 +987,69 @@ __device__ __forceinline__ void spmv_sell_pipe(const CsrArgs &A, const Gather &x
     if (s >= full) sell_slice<T, V, Epi, Gather>(A, x, epi, s);
 }
 
+// SELL with 2 rows per lane (variant bit 4096; slices of 128 rows): lane l
+// owns rows 128 s + 2 l and + 1, so each value and index access is one
+// 16-byte load (two rows' slot j, two rows' index word) — half the load
+// instructions per row of the 1-row form, which streams at 8 bytes per lane.
+// Same per-row sums in the same order. Gathers stay one 8-byte load per
+// entry.
+typedef unsigned long long Ull2 __attribute__((ext_vector_type(2)));
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void sell_slice2(const CsrArgs &A, const Gather &x, Epi &epi, int s) {
+  constexpr bool NT = (V & 2) != 0;
+  using PV = typename PairOf<T>::V;
+  const PV *__restrict__ sval = static_cast<const PV *>(A.sval);
+  const Ull2 *__restrict__ sidx = reinterpret_cast<const Ull2 *>(A.sidx);
+  const int lane = threadIdx.x & 63;
+  const SellSlice m = A.sl[s];
+  const int r0 = s * (2 * kSellRows) + 2 * lane;
+  const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
+  const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
+  epi.pre2(rc0, rc1);
+  const int dv = A.sdict[m.dict + lane];
+  T acc0 = T(0), acc1 = T(0);
+  for (int c = 0; c < m.width; c += 8) {
+    // voff and ioff are multiples of 128 entries / words: 16-byte aligned
+    const Ull2 iw = ldg<NT>(sidx + (m.ioff >> 1) + (int64_t)(c >> 3) * kSellRows + lane);
+    const PV *vp = sval + (m.voff >> 1) + (int64_t)c * kSellRows + lane;
+    PV v[8];
+    T g0[8], g1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ldg<NT>(vp + min(j, m.width - 1 - c) * kSellRows);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned k0 = (unsigned)(iw.x >> (8 * j)) & 0xffu;
+      const unsigned k1 = (unsigned)(iw.y >> (8 * j)) & 0xffu;
+      const int o0 = __builtin_amdgcn_ds_bpermute((int)(k0 << 2), dv);
+      const int o1 = __builtin_amdgcn_ds_bpermute((int)(k1 << 2), dv);
+      if constexpr ((V & 16) != 0) {
+        g0[j] = T(k0 & 1);
+        g1[j] = T(k1 & 1);
+      } else {
+        g0[j] = x(k0 != kSellPad ? r0 + o0 : rc0);
+        g1[j] = x(k1 != kSellPad ? r0 + 1 + o1 : rc1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned k0 = (unsigned)(iw.x >> (8 * j)) & 0xffu;
+      const unsigned k1 = (unsigned)(iw.y >> (8 * j)) & 0xffu;
+      const T t0 = acc0 + v[j].x * g0[j];
+      const T t1 = acc1 + v[j].y * g1[j];
+      acc0 = (k0 != kSellPad) ? t0 : acc0;
+      acc1 = (k1 != kSellPad) ? t1 : acc1;
+    }
+  }
+  epi.row2(r0, acc0, acc1, l0, l1);
+}
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sell2(const CsrArgs &A, const Gather &x, Epi &epi) {
+  int s, step, end;
+  sell_range((int)A.nsl, s, step, end);
+  for (; s < end; s += step) sell_slice2<T, V, Epi, Gather>(A, x, epi, s);
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
@@ -997,7 +1060,8 @@ using LdsOf = typename std::conditional<
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
                                          const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
-  if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
+  if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
+  else if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0) spmv_sell<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 256) != 0) spmv_rows_quad<T, V, Epi, Gather>(A, val, x, epi, sm);
@@ -1009,32 +1073,66 @@ __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__
 // Row epilogues: pre(i) loads the row's own operands early (the pipelined
 // loop issues it before the next block's prefetch, so waiting on it never
 // waits on the prefetch); row(i, s) consumes the row sum.
+// pre2 / row2: the same for two rows (SELL with 2 rows per lane); a row
+// past the matrix end is given clamped (pre2) and flagged dead (row2).
 template <typename T> struct EpiStore {
   T *__restrict__ y;
   __device__ __forceinline__ void pre(int) {}
   __device__ __forceinline__ void row(int i, T s) { y[i] = s; }
+  __device__ __forceinline__ void pre2(int, int) {}
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    if (l0) y[i] = s0;
+    if (l1) y[i + 1] = s1;
+  }
 };
 template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
   T *__restrict__ Ap;
   const T *__restrict__ p;
-  T acc, pv;
+  T acc, pv, pv1;
   __device__ __forceinline__ void pre(int i) { pv = p[i]; }
   __device__ __forceinline__ void row(int i, T s) {
     Ap[i] = s;
     acc += s * pv;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    pv = p[i0];
+    pv1 = p[i1];
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    if (l0) {
+      Ap[i] = s0;
+      acc += s0 * pv;
+    }
+    if (l1) {
+      Ap[i + 1] = s1;
+      acc += s1 * pv1;
+    }
   }
 };
 template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
   const T *__restrict__ b;
   T *__restrict__ r;
   T *__restrict__ p;
-  T acc, bv;
+  T acc, bv, bv1;
   __device__ __forceinline__ void pre(int i) { bv = b[i]; }
   __device__ __forceinline__ void row(int i, T s) {
     const T ri = bv - s;
     r[i] = ri;
     p[i] = ri;
     acc += ri * ri;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    bv = b[i0];
+    bv1 = b[i1];
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    if (l0) row(i, s0);
+    if (l1) {
+      const T ri = bv1 - s1;
+      r[i + 1] = ri;
+      p[i + 1] = ri;
+      acc += ri * ri;
+    }
   }
 };
 // Fused iteration k: p_k = r_k + beta_{k-1} p_{k-1} (CG.hpp:418 of body
@@ -1048,7 +1146,7 @@ template <typename T> struct EpiFused {
   T *__restrict__ Ap;
   T alpha, beta;
   bool do_x;
-  T acc, rv, pv, xv;
+  T acc, rv, pv, xv, rv1, pv1, xv1;
   __device__ __forceinline__ void pre(int i) {
     rv = r[i];
     pv = pp[i];
@@ -1061,11 +1159,27 @@ template <typename T> struct EpiFused {
     acc += s * pi;
     if (do_x) x[i] = xv + alpha * pv;
   }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    pre(i0);
+    rv1 = r[i1];
+    pv1 = pp[i1];
+    xv1 = x[i1];
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    if (l0) row(i, s0);
+    if (l1) {
+      const T pi = rv1 + beta * pv1;
+      pc[i + 1] = pi;
+      Ap[i + 1] = s1;
+      acc += s1 * pi;
+      if (do_x) x[i + 1] = xv1 + alpha * pv1;
+    }
+  }
 };
 template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
-  T acc0, acc1, bv, xv;
+  T acc0, acc1, bv, xv, bv1, xv1;
   __device__ __forceinline__ void pre(int i) {
     bv = b[i];
     xv = x[i];
@@ -1074,6 +1188,19 @@ template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
     const T a = bv - s;
     acc0 += a * a;
     acc1 += xv * xv;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    pre(i0);
+    bv1 = b[i1];
+    xv1 = x[i1];
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    if (l0) row(i, s0);
+    if (l1) {
+      const T a = bv1 - s1;
+      acc0 += a * a;
+      acc1 += xv1 * xv1;
+    }
   }
 };
 
@@ -1092,7 +1219,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
                                                     T *__restrict__ p, CgScalars<T> *st,
                                                     RedWs<T> *ws, T tol, long long cap) {
   __shared__ LdsOf<T, V> sm;
-  EpiInit<T> e{b, r, p, T(0), T(0)};
+  EpiInit<T> e{b, r, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
@@ -1115,7 +1242,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restr
                                                      int slot, RedWs<T> *ws) {
   if (!st->active[slot]) return;
   __shared__ LdsOf<T, V> sm;
-  EpiDot<T> e{Ap, p, T(0), T(0)};
+  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
   T v[1] = {e.acc};
   if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) st->pAp[slot] = v[0];
@@ -1142,7 +1269,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fused(CsrArgs A, const T *__res
   T v[1] = {T(0)};
   if (act) {
     const T beta = st->bodies == 0 ? T(0) : st->rr[prev] / st->rxr[prev];
-    EpiFused<T> e{r, pp, pc, x, Ap, alpha, beta, xp, T(0), T(0), T(0), T(0)};
+    EpiFused<T> e{r, pp, pc, x, Ap, alpha, beta, xp, T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
     spmv_any<T, V>(A, val, GatherP<T>{r, pp, beta}, e, sm);
     v[0] = e.acc;
   } else {
@@ -1179,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void k_accuracy(CsrArgs A, const T *__restr
                                                      const T *__restrict__ x, T *out2,
                                                      RedWs<T> *ws) {
   __shared__ LdsOf<T, V> sm;
-  EpiAccuracy<T> e{b, x, T(0), T(0), T(0), T(0)};
+  EpiAccuracy<T> e{b, x, T(0), T(0), T(0), T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
   T v[2] = {e.acc0, e.acc1};
   if (grid_reduce<T, 2>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
@@ -1385,23 +1512,23 @@ __global__ __launch_bounds__(kBlock) void k_gather(const T *__restrict__ src,
     dst[i] = src[idx[i]];
 }
 
-// SELL-64 values: slot j of row i = val[rowptr[i] + j], 0 past the row's end
+// SELL values: slot j of row i = val[rowptr[i] + j], 0 past the row's end
 // (those slots carry the padding index, the SpMV never multiplies them).
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_sell_pack(int64_t n, int64_t nsl,
+__global__ __launch_bounds__(kBlock) void k_sell_pack(int64_t n, int64_t nsl, int R,
                                                       const int *__restrict__ rowptr,
                                                       const T *__restrict__ val,
                                                       const SellSlice *__restrict__ sl,
                                                       T *__restrict__ sval) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nsl * kSellRows;
-       i += stride) {
-    const SellSlice m = sl[i / kSellRows];
-    const int l = (int)(i % kSellRows);
+  const int64_t H = (int64_t)kSellRows * R;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nsl * H; i += stride) {
+    const SellSlice m = sl[i / H];
+    const int li = (int)(i % H), l = li / R, r = li % R;
     const int a = i < n ? rowptr[i] : 0;
     const int len = i < n ? rowptr[i + 1] - a : 0;
     for (int j = 0; j < m.width; ++j)
-      sval[m.voff + (int64_t)j * kSellRows + l] = j < len ? val[a + j] : T(0);
+      sval[m.voff + ((int64_t)j * kSellRows + l) * R + r] = j < len ? val[a + j] : T(0);
   }
 }
 
@@ -1488,7 +1615,9 @@ constexpr int64_t kNtMinBytes = int64_t(256) << 20;
 template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   if (v < 0 && A.variant > 0) v = A.variant;  // chosen by cgx_csr_create's autotune
   if (v >= 0 && (v & 2048)) {
-    // pipelined SELL (bit 8) needs slices of at most 8 entries per row
+    // the variant follows the SELL copy's layout: bit 4096 for 2 rows per
+    // lane; pipelined (bit 8) for 1 row per lane and slices <= 8 wide
+    if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
     v = -1;  // no SELL copy: CSR-stream
   }
@@ -1558,6 +1687,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);                               \
     case 2056: CGX_LAUNCH_V(KERNEL, 2056, __VA_ARGS__);                               \
     case 2058: CGX_LAUNCH_V(KERNEL, 2058, __VA_ARGS__);                               \
+    case 6144: CGX_LAUNCH_V(KERNEL, 6144, __VA_ARGS__);                               \
+    case 6146: CGX_LAUNCH_V(KERNEL, 6146, __VA_ARGS__);                               \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -1590,6 +1721,8 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 2066: CGX_LAUNCH_V(k_spmv_dot, 2066, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 2072: CGX_LAUNCH_V(k_spmv_dot, 2072, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 2074: CGX_LAUNCH_V(k_spmv_dot, 2074, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 6160: CGX_LAUNCH_V(k_spmv_dot, 6160, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 6162: CGX_LAUNCH_V(k_spmv_dot, 6162, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -1664,8 +1797,12 @@ hipError_t Launch<T>::gather(const T *src, const int *idx, int64_t n, T *dst,
 
 template <typename T>
 hipError_t Launch<T>::sell_pack(const CsrDev &A, const T *val, T *sval, hipStream_t s) {
-  CGX_LAUNCH(k_sell_pack<T>, elem_grid(A.nsl * kSellRows, 4), A.n, A.nsl, A.rowptr, val, A.sl,
-             sval);
+  CGX_LAUNCH(k_sell_pack<T>, elem_grid(A.nsl * kSellRows * A.sell_r, 4), A.n, A.nsl, A.sell_r,
+             A.rowptr, val, A.sl, sval);
+}
+
+int launch_variant(const CsrDev &A, int dtype) {
+  return dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A);
 }
 
 template struct Launch<double>;

@@ -66,6 +66,9 @@ struct cgx_ctx {
   void *ws = nullptr;           // cgx::RedWs<double> (large enough for float)
   void *scratch = nullptr;      // 2 doubles for accuracy() results
   void *h_pinned = nullptr;     // pinned host staging (1 KiB: polls | host all-reduce)
+  // pinned ring for large host<->device copies (cgx_h2d / cgx_d2h), lazily
+  void *stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   // multi-GPU
   ncclComm *comm = nullptr;
   cgx::HostComm *host = nullptr;

@@ -75,8 +75,10 @@ int cgx_csr_info(cgx_csr *csr, int64_t *n, int64_t *nnz, int64_t *row_blocks,
 /* Rebuild the SpMV schedule for row blocks of `tile` entries (2048, the
  * default, or 1024 with at most 128 rows). Blocking. */
 int cgx_csr_set_tile(cgx_csr *csr, int tile);
-/* SpMV variant cgx_csr_create picked for this matrix by timing the candidate
- * kernels on the device ($CGX_SPMV_VARIANT overrides; 0 = size heuristic). */
+/* SpMV variant the matrix's launches use: the one cgx_csr_create picked by
+ * timing the candidate kernels on the device ($CGX_SPMV_VARIANT or
+ * cgx_csr_set_variant override), resolved against the matrix's layout
+ * (e.g. 6146 = SELL, 2 rows per lane, non-temporal loads). */
 int cgx_csr_variant(cgx_csr *csr, int *variant);
 /* Force the SpMV variant of this matrix (0: size heuristic). Variants with
  * bit 2048 use the SELL-64 copy cgx_csr_create builds for matrices whose
@@ -84,7 +86,11 @@ int cgx_csr_variant(cgx_csr *csr, int *variant);
  * with CGX_EUNSUPPORTED when the matrix has none (or it was freed because
  * the autotune chose a CSR-stream variant). */
 int cgx_csr_set_variant(cgx_csr *csr, int variant);
-/* 1 if the matrix holds a SELL-64 copy, else 0; its padded entry count. */
+/* Rebuild the SELL copy with 1 or 2 rows per lane (slices of 64 or 128
+ * rows), or drop it (0). A matrix that does not qualify ends without one.
+ * Blocking. */
+int cgx_csr_set_sell(cgx_csr *csr, int rows_per_lane);
+/* Rows per lane of the matrix's SELL copy (0: none); its padded entry count. */
 int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
@@ -204,13 +210,30 @@ int cgx_plan_remap(int64_t n_local, int64_t row_begin, int64_t nnz, int *col,
 int cgx_row_blocks(const int *h_rowptr, int64_t n, int64_t *nrb, int **rb,
                    int *max_row_nnz);
 void cgx_free_host(void *p);
-/* Host-only: the SELL-64 layout cgx_csr_create would build for a host CSR
- * (DESIGN.md §SpMV formats). *nsl = 0 when the matrix does not qualify.
+/* Host-only: the SELL layout (rows_per_lane 1 or 2) cgx_csr_create would
+ * build for a host CSR (DESIGN.md §SpMV formats). *nsl = 0 when the matrix
+ * does not qualify.
  * slices[4 q .. 4 q + 3] = {first value slot, first index word, first
  * dictionary entry, width} of slice q; dict[ndict] = the offset pool (col -
  * row), idx[nidx] = 8 one-byte dictionary indices per word (0xff: padding);
  * value_slots = length of the value array. Release with cgx_free_host. */
-int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+/* ---- Matrix-Market ingest / emit (test/mm_reader.cpp read_file) ---------
+ * cgx_mm_read: the reference loader's semantics (banner of 5 words, line 2
+ * always discarded, '%' lines skipped, a size line, "i j v" triplets until
+ * the first token that does not parse, off-diagonals always mirrored,
+ * entries sorted by (row, col), empty rows dropped from rowptr), parsed with
+ * `threads` threads (0: $OMP_NUM_THREADS or min(cores, 16)). Arrays are
+ * host memory; release with cgx_free_host. Replaces read_file
+ * (mm_reader.cpp:154-171).
+ * cgx_mm_write_lower: the lower triangle as a `symmetric` file with one
+ * comment line, values "%.17g" (reads back bit-identically). */
+int cgx_mm_read(const char *path, int threads, int64_t *n, int64_t *nnz, int **rowptr,
+                int **col, double **val);
+int cgx_mm_write_lower(const char *path, int64_t n, const int *rowptr, const int *col,
+                       const double *val, int threads);
+
+int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int rows_per_lane,
+                  int64_t *nsl,
                   int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,
                   unsigned long long **idx, int64_t *value_slots);
 

@@ -20,6 +20,7 @@ LIBD = os.path.join(ROOT, "conjugategradient_amd")
 REF_TEST = "/root/reference/test"
 GOLD = os.path.join(ROOT, "tests", "golden")
 TESTER = os.path.join(ROOT, "build", "dropin", "tester")
+TESTER_CGXREAD = os.path.join(ROOT, "build", "dropin", "tester_cgxread")
 EXAMPLE = os.path.join(ROOT, "build", "examples", "solve_poisson")
 
 
@@ -46,6 +47,24 @@ def test_reference_tester_compiles_unmodified(cxx, tmp_path):
         assert p.returncode != 0 and "cgx_create" in p.stderr
 
 
+def test_reference_tester_compiles_with_cgx_loader(tmp_path):
+    """Tester.cpp with examples/cgx_read_file.cpp in place of mm_reader.cpp."""
+    if not os.path.isdir(REF_TEST):
+        pytest.skip("reference sources not present (GPU box)")
+    out = str(tmp_path / "tester_cgxread")
+    r = _compile("g++", [os.path.join(REF_TEST, "Tester.cpp"),
+                         os.path.join(ROOT, "examples", "cgx_read_file.cpp")], out,
+                 ["-I" + REF_TEST])
+    assert r.returncode == 0, r.stderr
+    if not os.path.exists("/dev/kfd"):
+        # the loader runs on the host before the queue fails for lack of a device
+        p = subprocess.run([out, os.path.join(GOLD, "poisson2d_16.mtx")], capture_output=True,
+                           text=True)
+        assert p.returncode != 0 and "cgx_create" in p.stderr
+        p = subprocess.run([out, str(tmp_path / "missing.mtx")], capture_output=True, text=True)
+        assert p.returncode != 0 and "cannot open" in p.stderr
+
+
 def test_example_compiles(tmp_path):
     out = str(tmp_path / "solve_poisson")
     r = _compile("g++", [os.path.join(ROOT, "examples", "solve_poisson.cpp")], out,
@@ -59,11 +78,12 @@ def _parse(stdout):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("exe", [TESTER, TESTER_CGXREAD], ids=["mm_reader", "cgx_loader"])
 @pytest.mark.parametrize("name", ["poisson2d_16", "poisson2d_128", "poisson3d_16"])
-def test_reference_tester_runs_on_gpu(name):
-    if not os.path.exists(TESTER):
-        pytest.skip("build/dropin/tester not built (needs the reference sources at build time)")
-    p = subprocess.run([TESTER, os.path.join(GOLD, name + ".mtx")], capture_output=True,
+def test_reference_tester_runs_on_gpu(name, exe):
+    if not os.path.exists(exe):
+        pytest.skip(f"{exe} not built (needs the reference sources at build time)")
+    p = subprocess.run([exe, os.path.join(GOLD, name + ".mtx")], capture_output=True,
                        text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
     n, nnz, ms, acc = _parse(p.stdout)

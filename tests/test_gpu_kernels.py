@@ -261,3 +261,30 @@ def test_fused_split_runs(queue, oracle):
     for x in xs.values():
         np.testing.assert_array_equal(x, xs[(23,)])
     assert rel(xs[(23,)], xr) <= 1e-12
+
+
+@pytest.mark.parametrize("staged", ["1", "0"])
+def test_large_host_copies_round_trip(queue, monkeypatch, staged):
+    """cgx_h2d / cgx_d2h: device->host copies >= 16 MiB go through the pinned
+    ring (64 MiB chunks, $CGX_STAGED=0 turns it off); sizes that are not a
+    chunk multiple, unaligned pointers."""
+    import ctypes as C
+
+    from conjugategradient_amd._native import check, lib
+    monkeypatch.setenv("CGX_STAGED", staged)
+    L = lib()
+    nbytes = 150 * (1 << 20) + 13
+    src = np.random.default_rng(5).integers(0, 256, nbytes, dtype=np.uint8)
+    d = C.c_void_p()
+    check(L.cgx_alloc(queue.handle, nbytes, C.byref(d)))
+    try:
+        check(L.cgx_h2d(queue.handle, d, src.ctypes.data, nbytes))
+        out = np.zeros(nbytes, np.uint8)
+        check(L.cgx_d2h(queue.handle, out.ctypes.data, d, nbytes))
+        np.testing.assert_array_equal(out, src)
+        # an offset sub-range (unaligned pointers on both sides)
+        part = np.zeros(nbytes - 7, np.uint8)
+        check(L.cgx_d2h(queue.handle, part.ctypes.data, C.c_void_p(d.value + 7), nbytes - 7))
+        np.testing.assert_array_equal(part, src[7:])
+    finally:
+        L.cgx_free(queue.handle, d)

@@ -19,7 +19,7 @@ from tests.util import coo_to_csr, irregular_spd, rel
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [2048, 2050, 2056, 2058, 13, 15, 0]
+VARIANTS = [2048, 2050, 2056, 2058, 6144, 6146, 13, 15, 0]
 
 
 def banded(n, half=6, seed=1, empty_every=0):
@@ -66,15 +66,17 @@ def _sell_info(m):
     return has.value, padded.value
 
 
+@pytest.mark.parametrize("R", [1, 2])
 @pytest.mark.parametrize("case", ["poisson2d", "poisson3d_ragged", "banded", "empty_rows",
                                   "tiny"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype):
+def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype, R):
     rp, cl, vl = _matrix_cases(oracle)[case]
     n = len(rp) - 1
     A = Matrix(queue, vl, cl, rp, dtype=dtype)
+    check(lib().cgx_csr_set_sell(A.schedule(), R))
     has, padded = _sell_info(A)
-    assert has == 1, case
+    assert has == R, case
     assert len(vl) <= padded <= len(vl) + len(vl) // 4 + 4096 + 64 * np.diff(rp).max()
     x = np.random.default_rng(3).standard_normal(n)
     if dtype == np.float32:
@@ -111,6 +113,8 @@ def test_sell_not_built_for_scattered_matrix(queue):
     A = Matrix(queue, vl, cl, rp)
     has, _ = _sell_info(A)
     assert has == 0
+    check(lib().cgx_csr_set_sell(A.schedule(), 2))
+    assert _sell_info(A)[0] == 0
     with pytest.raises(CgxError, match="SELL"):
         check(lib().cgx_csr_set_variant(A.schedule(), 2048))
     with pytest.raises(CgxError, match="unknown"):
@@ -124,7 +128,8 @@ def test_sell_disabled_by_env(queue, oracle, monkeypatch):
     assert _sell_info(A)[0] == 0
 
 
-def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle):
+@pytest.mark.parametrize("R", [1, 2])
+def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle, R):
     # padding entries are dropped, not multiplied: an Inf/NaN in x reaches
     # exactly the rows whose real entries touch it, and -0 sums stay -0
     rp, cl, vl = oracle.poisson(2, 16, 12, 1)
@@ -134,6 +139,7 @@ def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle):
     x[77] = np.nan
     x[100] = -0.0
     A = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(A.schedule(), R))
     check(lib().cgx_csr_set_variant(A.schedule(), 2048))
     ops = VectorOperations(queue)
     ops.setVectorSize(n)
@@ -146,7 +152,7 @@ def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle):
     np.testing.assert_array_equal(np.signbit(y), np.signbit(ref))
 
 
-@pytest.mark.parametrize("sell", ["1", "0"])
+@pytest.mark.parametrize("sell", ["1", "2", "0"])
 @pytest.mark.parametrize("dim,n", [(2, 64), (3, 20)])
 def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     monkeypatch.setenv("CGX_SELL", sell)
@@ -158,7 +164,8 @@ def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     cg.solve(1e-8)
     v = C.c_int()
     check(lib().cgx_csr_variant(cg.A.schedule(), C.byref(v)))
-    assert bool(v.value & 2048) == (sell == "1")
+    assert bool(v.value & 2048) == (sell != "0")
+    assert _sell_info(cg.A)[0] == int(sell)
     xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-8)
     assert abs(cg.iterations - res.iterations) <= 2
     assert rel(cg.extract(), xr) <= 1e-10

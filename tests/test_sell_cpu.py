@@ -7,7 +7,8 @@ cgx_csr_create allocates:
   * index words: nidx;
   * dictionary pool: ndict;
   * gathered x: n.
-With values packed the way k_sell_pack packs them, the emulated row sums
+Both layouts are covered: 1 and 2 rows per lane. With values packed the
+way k_sell_pack packs them, the emulated row sums
 must equal the oracle's SpMV bit for bit.
 """
 import ctypes as C
@@ -22,7 +23,7 @@ ROWS = 64
 PAD = 0xFF
 
 
-def sell_plan(rp, cl):
+def sell_plan(rp, cl, R=1):
     L = lib()
     nsl, ndict, nidx, slots = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
     sl = C.POINTER(C.c_int64)()
@@ -30,7 +31,7 @@ def sell_plan(rp, cl):
     idx = C.POINTER(C.c_uint64)()
     rp = np.ascontiguousarray(rp, np.int32)
     cl = np.ascontiguousarray(cl, np.int32)
-    check(L.cgx_sell_plan(rp.ctypes.data, cl.ctypes.data, len(rp) - 1, C.byref(nsl), C.byref(sl),
+    check(L.cgx_sell_plan(rp.ctypes.data, cl.ctypes.data, len(rp) - 1, R, C.byref(nsl), C.byref(sl),
                           C.byref(ndict), C.byref(dic), C.byref(nidx), C.byref(idx),
                           C.byref(slots)))
     if nsl.value == 0:
@@ -44,51 +45,57 @@ def sell_plan(rp, cl):
     return out
 
 
-def pack_values(rp, vl, sl, slots):
+def pack_values(rp, vl, sl, slots, R=1):
     """k_sell_pack: slot j of row i = val[rowptr[i] + j], 0 past the row."""
     n = len(rp) - 1
-    sval = np.zeros(slots + 8 * ROWS, vl.dtype)
+    sval = np.zeros(slots + 8 * ROWS * R, vl.dtype)
+    H = ROWS * R
     for q, (voff, _, _, w) in enumerate(sl):
-        for l in range(ROWS):
-            i = q * ROWS + l
+        for li in range(H):
+            i = q * H + li
             if i >= n:
                 continue
+            l, r = divmod(li, R)
             a, e = rp[i], rp[i + 1]
             for j in range(e - a):
-                sval[voff + j * ROWS + l] = vl[a + j]
+                sval[voff + (j * ROWS + l) * R + r] = vl[a + j]
     return sval
 
 
-def emulate_spmv(rp, sl, dic, idx, sval, x):
-    """spmv_sell, with every index the kernel forms checked against the
-    array extents cgx_csr_create allocates."""
+def emulate_spmv(rp, sl, dic, idx, sval, x, R=1):
+    """spmv_sell (R = 1) / sell_slice2 (R = 2), with every index the kernel
+    forms checked against the array extents cgx_csr_create allocates."""
     n = len(rp) - 1
     y = np.zeros(n)
     lane = np.arange(ROWS)
+    H = ROWS * R
+    if R == 2:   # 16-byte loads: voff / ioff must be even (aligned)
+        assert (sl[:, 0] % 2 == 0).all() and (sl[:, 1] % 2 == 0).all()
     for q, (voff, ioff, dbase, w) in enumerate(sl):
-        row = q * ROWS + lane
-        live = row < n
-        rowc = np.where(live, row, n - 1)
         assert dbase + ROWS <= len(dic)
         dv = dic[dbase + lane]
-        acc = np.zeros(ROWS)
-        for c in range(0, w, 8):
-            wi = ioff + (c >> 3) * ROWS + lane
-            assert wi.max() < len(idx)
-            iw = idx[wi]
-            for j in range(8):
-                vi = voff + (c + j) * ROWS + lane
-                assert vi.max() < len(sval)
-                v = sval[vi]
-                k = ((iw >> np.uint64(8 * j)) & np.uint64(0xFF)).astype(np.int64)
-                off = dv[(k * 4 // 4) % ROWS]              # ds_bpermute
-                g_idx = np.where(k != PAD, row + off, rowc)
-                assert g_idx.min() >= 0 and g_idx.max() < n
-                g = x[g_idx]
-                with np.errstate(invalid="ignore"):
-                    t = acc + v * g
-                acc = np.where(k != PAD, t, acc)
-        y[row[live]] = acc[live]
+        for r in range(R):
+            row = q * H + R * lane + r
+            live = row < n
+            rowc = np.where(live, row, n - 1)
+            acc = np.zeros(ROWS)
+            for c in range(0, w, 8):
+                wi = ioff + ((c >> 3) * ROWS + lane) * R + r
+                assert wi.max() < len(idx)
+                iw = idx[wi]
+                for j in range(8):
+                    vi = voff + ((c + min(j, w - 1 - c)) * ROWS + lane) * R + r
+                    assert vi.max() < len(sval)
+                    v = sval[vi]
+                    k = ((iw >> np.uint64(8 * j)) & np.uint64(0xFF)).astype(np.int64)
+                    off = dv[(k * 4 // 4) % ROWS]              # ds_bpermute
+                    g_idx = np.where(k != PAD, row + off, rowc)
+                    assert g_idx.min() >= 0 and g_idx.max() < n
+                    g = x[g_idx]
+                    with np.errstate(invalid="ignore"):
+                        t = acc + v * g
+                    acc = np.where(k != PAD, t, acc)
+            y[row[live]] = acc[live]
     return y
 
 
@@ -105,23 +112,24 @@ def cases(oracle):
     }
 
 
+@pytest.mark.parametrize("R", [1, 2])
 @pytest.mark.parametrize("case", ["poisson3d_ragged", "poisson2d", "banded", "empty_rows",
                                   "tiny", "wide"])
-def test_sell_layout_in_bounds_and_bitexact(oracle, case):
+def test_sell_layout_in_bounds_and_bitexact(oracle, case, R):
     rp, cl, vl = cases(oracle)[case]
-    plan = sell_plan(rp, cl)
+    plan = sell_plan(rp, cl, R)
     assert plan is not None, case
     sl, dic, idx, slots = plan
     n = len(rp) - 1
-    assert len(sl) == (n + ROWS - 1) // ROWS
-    assert (sl[:, 3] <= 64).all() and slots == (sl[:, 3] * ROWS).sum()
+    assert len(sl) == (n + ROWS * R - 1) // (ROWS * R)
+    assert (sl[:, 3] <= 64).all() and slots == (sl[:, 3] * ROWS * R).sum()
     # dictionary indices < 64, every real entry present exactly once
     b = idx.view(np.uint8)
     assert ((b == PAD) | (b < 64)).all()
     assert (b != PAD).sum() == len(vl)
-    sval = pack_values(rp, vl, sl, slots)
+    sval = pack_values(rp, vl, sl, slots, R)
     x = np.random.default_rng(1).standard_normal(n)
-    np.testing.assert_array_equal(emulate_spmv(rp, sl, dic, idx, sval, x),
+    np.testing.assert_array_equal(emulate_spmv(rp, sl, dic, idx, sval, x, R),
                                   oracle.spmv(rp, cl, vl, x))
 
 
@@ -135,6 +143,6 @@ def test_sell_dictionaries_are_shared(oracle):
 
 def test_sell_rejects_scattered_and_long_rows():
     rp, cl, _ = irregular_spd(20_000, seed=4)
-    assert sell_plan(rp, cl) is None
+    assert sell_plan(rp, cl) is None and sell_plan(rp, cl, 2) is None
     rp, cl, _ = irregular_spd(5_000, seed=5, hub=3000)   # one row of ~3000 entries
     assert sell_plan(rp, cl) is None

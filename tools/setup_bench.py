@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Setup-path timings: host->device upload of a 256^3
+CSR (1.47 GB) through the pinned ring vs a single hipMemcpy, download, and
+cgx_csr_create (row-block schedule + SELL copy + SpMV autotune).
+
+    python tools/setup_bench.py [--grid 256]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import conjugategradient_amd as cga  # noqa: E402
+from conjugategradient_amd._native import check, lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=256)
+    a = ap.parse_args()
+    L = lib()
+    q = cga.Queue(0)
+    m = cga.Matrix.poisson(q, 3, a.grid, a.grid, a.grid)
+    rows, cols, data = m.rows().download(), m.columns().download(), m.data().download()
+    nbytes = rows.nbytes + cols.nbytes + data.nbytes
+    out = {"grid": a.grid, "csr_bytes": nbytes}
+    for staged in ("0", "1", "0", "1"):
+        os.environ["CGX_STAGED"] = staged
+        t = time.perf_counter()
+        A = cga.Matrix(q, data, cols, rows)
+        dt = time.perf_counter() - t
+        out.setdefault(f"h2d_GBps_staged{staged}", []).append(round(nbytes / dt / 1e9, 2))
+        t = time.perf_counter()
+        A.data().download()
+        dt = time.perf_counter() - t
+        out.setdefault(f"d2h_GBps_staged{staged}", []).append(round(data.nbytes / dt / 1e9, 2))
+        del A
+    os.environ.pop("CGX_STAGED", None)
+    for sell in ("0", "2"):
+        os.environ["CGX_SELL"] = sell
+        t = time.perf_counter()
+        h = C.c_void_p()
+        check(L.cgx_csr_create(q.handle, m.N(), m.NNZ(), m.rows().ptr, m.columns().ptr,
+                               m.data().ptr, 0, rows.ctypes.data, C.byref(h)))
+        out[f"csr_create_s_sell{sell}"] = round(time.perf_counter() - t, 3)
+        v = C.c_int()
+        check(L.cgx_csr_variant(h, C.byref(v)))
+        out[f"variant_sell{sell}"] = v.value
+        L.cgx_csr_destroy(h)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

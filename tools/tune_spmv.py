@@ -61,13 +61,20 @@ def main():
         check(L.cgx_csr_create(q.handle, n, nnz, A.rows().ptr, A.columns().ptr, A.data().ptr, 0,
                                None, C.byref(wave)))
         check(L.cgx_csr_set_tile(wave, 512))
+        pair = None  # SELL with 2 rows per lane for the variants with bit 4096
+        if any(v & 4096 for v in variants):
+            pair = C.c_void_p()
+            check(L.cgx_csr_create(q.handle, n, nnz, A.rows().ptr, A.columns().ptr,
+                                   A.data().ptr, 0, None, C.byref(pair)))
+            check(L.cgx_csr_set_sell(pair, 2))
         x = cga.Vector(q, np.random.default_rng(0).standard_normal(n))
         ys = {v: cga.Vector(q, n) for v in variants}
         times = {v: [] for v in variants}
         for _ in range(a.rounds):
             for v in variants:
                 ms = C.c_double(0)
-                sched = wave if v & 512 else half if v & 64 else A.schedule()
+                sched = (pair if v & 4096 else wave if v & 512 else half if v & 64
+                         else A.schedule())
                 check(L.cgx_tune_spmv(q.handle, sched, v, x.ptr(), ys[v].ptr(), a.iters,
                                       C.byref(ms)))
                 times[v].append(ms.value)
@@ -83,6 +90,8 @@ def main():
                               "bitexact_vs_v0": same}), flush=True)
         L.cgx_csr_destroy(half)
         L.cgx_csr_destroy(wave)
+        if pair is not None:
+            L.cgx_csr_destroy(pair)
         del A, x, ys
 
 
