@@ -214,8 +214,11 @@ def main():
         if os.path.exists(pmc):
             try:
                 meta = json.load(open(pmc))
-                if meta.get("grid") == n3 and meta.get("n_gpus", 1) == 1:
+                # PMC bytes of this very kernel: same per-GPU grid, variant, mode
+                if (meta.get("grid") == n3 and meta.get("spmv_variant") == variant.value
+                        and meta.get("kernel") == roof["kernel"]):
                     roof["traffic"] = meta.get("hbm_bytes_per_launch")
+                    roof["traffic_source"] = "profiles/pmc_spmv_dot.json"
             except Exception:
                 pass
 
