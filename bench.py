@@ -74,9 +74,9 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
-    ap.add_argument("--mode", type=int, choices=[0, 1, 2], default=0,
-                    help="iteration structure (cgx_cg_set_mode): 0 auto (= 1), 1 three "
-                         "kernels, 2 fused (single GPU)")
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3], default=0,
+                    help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
+                         "2 fused (single GPU), 3 three kernels with the x update deferred")
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="N>1 collectives: RCCL (default) or the host-staged test transport "
                          "(lets ranks share one GPU; rehearsal only, numbers meaningless)")
@@ -247,7 +247,9 @@ def main():
                        "rows_global": n_global, "nnz_global": nnz_global,
                        "bytes_per_iteration": b_alg(n_global, nnz_global),
                        "parallelism": f"rows{world}" if world > 1 else "single",
-                       "iteration": "fused (2 kernels)" if fused else "3 kernels",
+                       "iteration": {0: "3 kernels, x update deferred over 4 bodies (auto)",
+                                     1: "3 kernels", 2: "fused (2 kernels)",
+                                     3: "3 kernels, x update deferred over 4 bodies"}[args.mode],
                        "spmv_variant": int(variant.value)},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -36,6 +36,14 @@ template <typename T> struct CgScalars {
   long long cap;     // max bodies: N+1 (CG.hpp:436) or a caller cap
   int stopped;       // 0 running, 1 stop rule (tol / NaN), 2 cap reached
   int pad_i;
+  // deferred x update (mode 3, cgx_abi.cpp enqueue_iter_defer): alpha of the
+  // body in slot s, set by its update_r; ran[s]: the body ran and its x
+  // update is not applied yet (set by its update_xp, cleared by the slot-3
+  // flush); skip[s]: an end-of-run flush already applied it (cleared by the
+  // body's update_r). Each is written and read by different launches.
+  T alpha[4];
+  int ran[4];
+  int skip[4];
 };
 
 // Grid-reduction workspace. Arrivals are sharded over kRedGroups tickets
@@ -113,6 +121,10 @@ template <typename T> struct Launch {
                             RedWs<T> *ws, hipStream_t s);
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
                               int slot, hipStream_t s);
+  static hipError_t update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
+                                   const T *r, CgScalars<T> *st, int slot, hipStream_t s);
+  static hipError_t flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
+                                hipStream_t s);
   static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,
                             hipStream_t s);
   static hipError_t axpby(int mode, int64_t n, const T *x, const T *y, const T *a,

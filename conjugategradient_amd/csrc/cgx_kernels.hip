@@ -1229,6 +1229,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
     st->active[0] = 1;
     st->active[1] = st->active[2] = st->active[3] = 0;
     st->xpend[0] = st->xpend[1] = st->xpend[2] = st->xpend[3] = 0;
+    for (int t = 0; t < 4; ++t) st->ran[t] = st->skip[t] = 0;
     st->bodies = 0;
     st->cap = cap;
     st->stopped = 0;
@@ -1337,6 +1338,10 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
   __shared__ T red[4];
   __shared__ int flag;
   const T alpha = st->rxr[slot] / st->pAp[slot];
+  if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // for the deferred x update
+    st->alpha[slot] = alpha;
+    st->skip[slot] = 0;
+  }
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -1597,6 +1602,148 @@ template <typename T> int Launch<T>::grid_rows(int nrb) {
 }
 template <typename T> int Launch<T>::grid_elems(int64_t n) { return elem_grid(n, 8); }
 
+
+// Deferred-x iteration (mode 3), kernel 3 of 3 for body k in slot s:
+// p_{k+1} = r + beta p_k into the next of four p buffers (CG.hpp:418) and
+// the stop rule (CG.hpp:396-404, 410-417, 436) as in k_update_xp, but the x
+// update (CG.hpp:390) is applied once per four bodies: in slot 3 (FLUSH),
+// x = (((x + a0 p0) + a1 p1) + a2 p2) + a3 p3 over the slots an end-of-run
+// flush has not applied yet — per element the same rounded operations in
+// the same order as four in-place updates, so x is bit-identical, for
+// 8 N + 8 N (x) + 24 N (p0..p2) bytes once instead of 16 N four times.
+// In slot 3, pn is P0 (p_{k+1} replaces p_{k-3}): every element's flush
+// operands are loaded before its stores, and pn / P0 carry no __restrict__.
+template <typename T, bool FLUSH>
+__global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restrict__ x,
+                                                           const T *p, T *pn, const T *P0,
+                                                           const T *P1, const T *P2,
+                                                           const T *__restrict__ r,
+                                                           CgScalars<T> *st, int slot) {
+  const int nxt = (slot + 1) & 3;
+  if (!st->active[slot]) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
+    return;
+  }
+  const T rxr = st->rxr[slot];
+  const T rr = st->rr[slot];
+  const T beta = rr / rxr;
+  // slot-3 flush: alphas and skips of the group, written by earlier launches
+  T a[4] = {T(0), T(0), T(0), T(0)};
+  bool use[4] = {false, false, false, false};
+  if constexpr (FLUSH) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      a[t] = st->alpha[t];
+      use[t] = st->skip[t] == 0;
+    }
+  }
+  using V = typename Vec2<T>::V;
+  const int64_t n2 = n >> 1;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const V *p2 = reinterpret_cast<const V *>(p);
+  V *pn2 = reinterpret_cast<V *>(pn);
+  const V *rv2 = reinterpret_cast<const V *>(r);
+  V *x2 = reinterpret_cast<V *>(x);
+  const V *Q[3] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
+                   reinterpret_cast<const V *>(P2)};
+  auto body = [&](int64_t i) {
+    const V pv = p2[i];
+    const V rv = rv2[i];
+    V q[3], xv;
+    if constexpr (FLUSH) {
+      xv = x2[i];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) q[t] = Q[t][i];  // before pn (= P0) is written
+    }
+    V o;
+    o.x = rv.x + beta * pv.x;
+    o.y = rv.y + beta * pv.y;
+    if constexpr (FLUSH) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        if (use[t]) {
+          xv.x = xv.x + a[t] * q[t].x;
+          xv.y = xv.y + a[t] * q[t].y;
+        }
+      }
+      if (use[3]) {
+        xv.x = xv.x + a[3] * pv.x;
+        xv.y = xv.y + a[3] * pv.y;
+      }
+      x2[i] = xv;
+    }
+    pn2[i] = o;
+  };
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(i + u * stride);
+  }
+  for (; i < n2; i += stride) body(i);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (n & 1) {
+      const T pv = p[n - 1];
+      if constexpr (FLUSH) {
+        T xv = x[n - 1];
+        const T *Ps[4] = {P0, P1, P2, p};
+        for (int t = 0; t < 4; ++t)
+          if (use[t]) xv = xv + a[t] * Ps[t][n - 1];
+        x[n - 1] = xv;
+      }
+      pn[n - 1] = r[n - 1] + beta * pv;
+    }
+    // stop rule, as k_update_xp
+    const long long m = st->bodies + 1;
+    st->bodies = m;
+    const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
+    const bool cont = !cond && m < st->cap;
+    st->active[nxt] = cont ? 1 : 0;
+    st->rxr[nxt] = rr;
+    st->stopped = cond ? 1 : (cont ? 0 : 2);
+    if constexpr (FLUSH) {
+      for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+    } else {
+      st->ran[slot] = 1;
+    }
+  }
+}
+
+// End of a run in mode 3: apply the bodies of the current group that ran and
+// were not applied yet, in slot order. k_mark_defer then marks them applied
+// (a separate launch: the workgroups here read the marks).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_flush_defer(int64_t n, T *__restrict__ x,
+                                                        const T *__restrict__ P0,
+                                                        const T *__restrict__ P1,
+                                                        const T *__restrict__ P2,
+                                                        const T *__restrict__ P3,
+                                                        const CgScalars<T> *st) {
+  T a[4];
+  bool use[4];
+  bool any = false;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    a[t] = st->alpha[t];
+    use[t] = st->ran[t] != 0 && st->skip[t] == 0;
+    any = any || use[t];
+  }
+  if (!any) return;
+  const T *Ps[4] = {P0, P1, P2, P3};
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    T xv = x[i];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (use[t]) xv = xv + a[t] * Ps[t][i];
+    x[i] = xv;
+  }
+}
+
+template <typename T> __global__ void k_mark_defer(CgScalars<T> *st) {
+  for (int t = 0; t < 4; ++t)
+    if (st->ran[t]) st->skip[t] = 1;
+}
+
 #define CGX_LAUNCH(kernel, grid, ...)                                              \
   do {                                                                             \
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, s, __VA_ARGS__);       \
@@ -1754,6 +1901,27 @@ template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
                                 int slot, hipStream_t s) {
   CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot);
+}
+template <typename T>
+hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
+                                     const T *r, CgScalars<T> *st, int slot, hipStream_t s) {
+  if (slot == 3) {
+    CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n), n, x, p, pn, (const T *)P[0],
+               (const T *)P[1], (const T *)P[2], r, st, slot);
+  }
+  CGX_LAUNCH((k_update_p_defer<T, false>), grid_elems(n), n, x, p, pn, (const T *)P[0],
+             (const T *)P[1], (const T *)P[2], r, st, slot);
+}
+template <typename T>
+hipError_t Launch<T>::flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(k_flush_defer<T>, dim3(elem_grid(n, 4)), dim3(kBlock), 0, s, n, x,
+                     (const T *)P[0], (const T *)P[1], (const T *)P[2], (const T *)P[3],
+                     (const CgScalars<T> *)st);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_mark_defer<T>, dim3(1), dim3(1), 0, s, st);
+  return hipGetLastError();
 }
 template <typename T>
 hipError_t Launch<T>::dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,

@@ -139,12 +139,15 @@ int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable);
 int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
 /* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
 int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
-/* Iteration structure (before cgx_cg_begin): 0 auto (= 1), 1 three kernels
+/* Iteration structure (before cgx_cg_begin): 0 auto (= 3, the default), 1
+ * three kernels
  * (SpMV+p.Ap, r-update+r.r, x/p-update), 2 fused (single device only): two
  * kernels, the x/p update folded into the next iteration's SpMV (p_j =
  * r_j + beta p_old_j computed in the gather), 8 bytes/row less traffic but
- * twice the gathers; measured no faster on MI355X. Both modes
- * give bit-identical x. */
+ * twice the gathers; 3 three kernels with the x update deferred: p cycles
+ * through four buffers and x += a0 p0 + ... + a3 p3 (in order) runs once
+ * per four bodies and at the end of each cgx_cg_run (34 N instead of 40 N
+ * bytes per body for the x/p update). All modes give bit-identical x. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
 
 /* CG::accuracy (CG.hpp:463-515): blocking; |sum (b-Ax)^2 / sum x^2|. */

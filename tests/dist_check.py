@@ -3,7 +3,7 @@
 rank, launched with torch.distributed.run:
 
   python -m torch.distributed.run --nproc-per-node W --master-addr 127.0.0.1 \
-      --master-port P tools/dist_check.py [--grid 32] [--tol 1e-8]
+      --master-port P tests/dist_check.py [--grid 32] [--tol 1e-8] [--mode 3]
 
 Rank r drives device (LOCAL_RANK % visible devices), so W ranks can share
 one GPU when the communication library allows it. The global 3-D Poisson
@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--grid", type=int, default=32)
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl")
+    ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -79,6 +80,7 @@ def main():
     x.fill(0.0)
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+    check(L.cgx_cg_set_mode(cg, a.mode))
     bodies, rxr = C.c_int64(), C.c_double()
     check(L.cgx_cg_solve(cg, b.ptr, x.ptr, a.tol, -1, C.byref(bodies), C.byref(rxr)))
     acc = C.c_double()
@@ -92,7 +94,7 @@ def main():
         xr, res = O.cg_solve(rp, cl, vl, np.arange(1, n + 1, dtype=np.float64), a.tol)
         relerr = float(np.linalg.norm(xg - xr) / np.linalg.norm(xr))
         ok = relerr <= 1e-10 and abs(bodies.value - res.iterations) <= 2
-        print(json.dumps({"world": world, "transport": a.transport, "grid": g, "bodies": bodies.value,
+        print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode, "grid": g, "bodies": bodies.value,
                           "oracle_bodies": res.iterations, "rel_err": relerr,
                           "accuracy": acc.value, "ghosts": [p[1] for p in parts],
                           "neighbours": [p[2] for p in parts], "ok": ok}), flush=True)

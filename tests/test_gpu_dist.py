@@ -5,7 +5,7 @@ runs use the host-staged transport (cgx_dist_init_host over gloo): the same
 halo plan, ghost area, pack kernel, all-reduce points and stop rule as the
 RCCL path, only the bytes travel through host memory. The RCCL transport
 itself runs at world size 1 here and at 1/2/4/8 in the driver's scaling
-bench (bench.py). Each run is a tools/dist_check.py job under
+bench (bench.py). Each run is a tests/dist_check.py job under
 torch.distributed.run; rank 0 compares x with the oracle (rel 1e-10,
 bodies +-2)."""
 import json
@@ -28,21 +28,22 @@ def _port():
     return p
 
 
-def _run(nproc, transport, grid):
+def _run(nproc, transport, grid, mode=0):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "tools", "dist_check.py"), "--transport", transport,
-           "--grid", str(grid)]
+           os.path.join(ROOT, "tests", "dist_check.py"), "--transport", transport,
+           "--grid", str(grid), "--mode", str(mode)]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     return json.loads(line)
 
 
-@pytest.mark.parametrize("nproc,transport,grid", [(1, "rccl", 32), (2, "host", 24),
-                                                  (3, "host", 20)])
-def test_partitioned_solve_matches_oracle(nproc, transport, grid):
-    r = _run(nproc, transport, grid)
+@pytest.mark.parametrize("nproc,transport,grid,mode", [(1, "rccl", 32, 0), (2, "host", 24, 0),
+                                                       (3, "host", 20, 0), (2, "host", 20, 3),
+                                                       (1, "rccl", 24, 3)])
+def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
+    r = _run(nproc, transport, grid, mode)
     assert r["ok"], r
     if nproc > 1:
         # slab partition of a 3-D grid: every rank has ghosts, inner ranks 2 nbrs

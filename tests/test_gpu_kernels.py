@@ -201,7 +201,7 @@ def test_errors(queue):
 
 def _run_modes(rp, cl, vl, b, tol, max_iter=-1, poll=32, graph=True):
     out = {}
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         cg = cga.CG.createCG()
         cg.mode = mode
         cg.poll_every = poll
@@ -216,8 +216,9 @@ def _run_modes(rp, cl, vl, b, tol, max_iter=-1, poll=32, graph=True):
 @pytest.mark.parametrize("case,tol,poll,graph", [("p2d", 1e-8, 32, True), ("p3d", 1e-24, 8, False),
                                                   ("irr", 1e-6, 4, True), ("p2d", 0.0, 32, True)])
 def test_fused_iteration_bit_identical_to_three_kernels(oracle, case, tol, poll, graph):
-    """Mode 2 folds the x/p update into the next SpMV; every value it computes
-    is the same expression as mode 1's, so x is bit-identical."""
+    """Mode 2 folds the x/p update into the next SpMV, mode 3 defers the x
+    update to every fourth body; every value either computes is the same
+    expression, in the same order, as mode 1's, so x is bit-identical."""
     if case == "p2d":
         rp, cl, vl = oracle.poisson(2, 48, 40, 1)
     elif case == "p3d":
@@ -226,15 +227,19 @@ def test_fused_iteration_bit_identical_to_three_kernels(oracle, case, tol, poll,
         rp, cl, vl = irregular_spd(20_000, seed=4)
     b = np.arange(1, len(rp), dtype=np.float64)
     out = _run_modes(rp, cl, vl, b, tol, poll=poll, graph=graph)
-    (x1, it1, r1), (x2, it2, r2) = out[1], out[2]
-    assert it1 == it2
-    np.testing.assert_array_equal(x1, x2)
-    assert r1 == r2 or (np.isnan(r1) and np.isnan(r2))
+    x1, it1, r1 = out[1]
+    for mode in (2, 3):
+        x2, it2, r2 = out[mode]
+        assert it1 == it2, mode
+        np.testing.assert_array_equal(x1, x2, err_msg=f"mode {mode}")
+        assert r1 == r2 or (np.isnan(r1) and np.isnan(r2))
 
 
-def test_fused_split_runs(queue, oracle):
+@pytest.mark.parametrize("mode", [2, 3])
+def test_fused_split_runs(queue, oracle, mode):
     """begin + several cgx_cg_run calls (each ends with the pending-x flush)
-    equals one run, and the oracle capped at the same count."""
+    equals one run, and the oracle capped at the same count. The splits end
+    runs in every slot of mode 3's 4-body groups."""
     import ctypes as C
     from conjugategradient_amd._native import check, lib
     rp, cl, vl = oracle.poisson(2, 30, 30, 1)
@@ -244,11 +249,11 @@ def test_fused_split_runs(queue, oracle):
     bv = Vector(queue, b)
     L = lib()
     xs = {}
-    for split in ((23,), (5, 1, 17), (7, 16)):
+    for split in ((23,), (5, 1, 17), (7, 16), (1, 1, 1, 1, 2, 3, 14), (4, 8, 11)):
         xv = Vector(queue, n)
         h = C.c_void_p()
         check(L.cgx_cg_create(queue.handle, A.schedule(), C.byref(h)))
-        check(L.cgx_cg_set_mode(h, 2))
+        check(L.cgx_cg_set_mode(h, mode))
         check(L.cgx_cg_config(h, 4, 1))
         check(L.cgx_cg_begin(h, bv.ptr(), xv.ptr(), 0.0, 1000))
         tot, st = C.c_int64(), C.c_int()
