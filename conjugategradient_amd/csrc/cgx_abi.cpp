@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <tuple>
 #include <thread>
 #include <vector>
 
@@ -628,7 +629,8 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 }
 
 void free_sell(cgx_csr *A) {
-  for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val}) {
+  for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
+                   &A->d_sell_order}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -637,6 +639,7 @@ void free_sell(cgx_csr *A) {
   A->dev.sidx = nullptr;
   A->dev.sval = nullptr;
   A->dev.nsl = 0;
+  A->dev.sorder = nullptr;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
   A->sell_padded = 0;
@@ -751,6 +754,33 @@ extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, i
   return CGX_OK;
 }
 
+// Visit order of the slices. P is the stride of the farthest
+// band (the largest |col - row|: a z-plane of a 3-D stencil). Within each
+// XCD's eighth of the slices (the kernel's sell_range split), chunks of 128
+// slices of a plane are walked through all the planes before the next
+// chunk. The slices in flight on an XCD (1024 waves) then span ~8 planes of
+// one chunk, and the p rows they gather (~1.3 MB at 256^3) stay in the
+// XCD's 4 MB L2, where plane-by-plane order spans two whole planes and
+// re-fetches p. Empty when planes are small (< 256 slices).
+static std::vector<int> sell_visit_order(int64_t nsl, int64_t H, int64_t P) {
+  constexpr int64_t kChunk = 128;
+  std::vector<int> order;
+  if (P / H < 2 * kChunk) return order;
+  order.resize((size_t)nsl);
+  std::vector<std::tuple<int64_t, int64_t, int64_t, int>> key;
+  for (int g = 0; g < 8; ++g) {
+    const int64_t lo = (nsl * g) >> 3, hi = (nsl * (g + 1)) >> 3;
+    key.clear();
+    for (int64_t q = lo; q < hi; ++q) {
+      const int64_t r0 = q * H, z = r0 / P, u = (r0 % P) / H;
+      key.emplace_back(u / kChunk, z, u, (int)q);
+    }
+    std::sort(key.begin(), key.end());
+    for (size_t i = 0; i < key.size(); ++i) order[(size_t)lo + i] = std::get<3>(key[i]);
+  }
+  return order;
+}
+
 // SELL copy of A on the device with R rows per lane (0: the default layout),
 // when the matrix qualifies (sell_plan_host); otherwise A keeps only the
 // CSR-stream schedule and this returns CGX_OK. Errors are device failures
@@ -808,6 +838,27 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   if (e != hipSuccess) {
     free_sell(A);
     return hip_fail(e, "cgx_csr_create(SELL copy)");
+  }
+  // visit order, opt-in ($CGX_SELL_ORDER=1): it measured no faster at 256^3
+  // (the re-fetched p lines are Infinity-Cache hits)
+  {
+    int64_t P = 0;
+    for (int v : pool) P = std::max<int64_t>(P, v < 0 ? -(int64_t)v : v);
+    const char *env = std::getenv("CGX_SELL_ORDER");
+    std::vector<int> order;
+    if (env && std::atoi(env) == 1) order = sell_visit_order(nsl, (int64_t)kSellRows * R, P);
+    if (!order.empty()) {
+      e = hipMalloc(&A->d_sell_order, order.size() * sizeof(int));
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(A->d_sell_order, order.data(), order.size() * sizeof(int),
+                           hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) {
+        free_sell(A);
+        return hip_fail(e, "cgx_csr_create(SELL order)");
+      }
+      A->dev.sorder = (const int *)A->d_sell_order;
+    }
   }
   A->dev.sl = (const SellSlice *)A->d_sell_sl;
   A->dev.sdict = (const int *)A->d_sell_dict;

@@ -100,6 +100,7 @@ struct CsrDev {
   int64_t nsl = 0;
   int sell_maxw = 0;  // widest slice
   int sell_r = 1;     // rows per lane of the SELL copy
+  const int *sorder = nullptr;  // visit order of the slices (null: index order)
 };
 
 template <typename T> struct Launch {

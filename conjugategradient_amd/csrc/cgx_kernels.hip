@@ -195,6 +195,7 @@ struct CsrArgs {
   const unsigned long long *__restrict__ sidx;
   const void *sval;
   int64_t nsl;
+  const int *__restrict__ sorder;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -903,11 +904,19 @@ __device__ __forceinline__ void sell_slice(const CsrArgs &A, const Gather &x, Ep
   if (live) epi.row(row, acc);
 }
 
+// The k-th slice to visit: A.sorder[k] where the host built a visit order
+// (cgx_abi.cpp sell_visit_order), else k. Wave-uniform scalar load.
+__device__ __forceinline__ int slice_at(const CsrArgs &A, int k) {
+  if (!A.sorder) return k;
+  return ((const __attribute__((address_space(4))) int *)A.sorder)
+      [__builtin_amdgcn_readfirstlane(k)];
+}
+
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell(const CsrArgs &A, const Gather &x, Epi &epi) {
   int s, step, end;
   sell_range((int)A.nsl, s, step, end);
-  for (; s < end; s += step) sell_slice<T, V, Epi, Gather>(A, x, epi, s);
+  for (; s < end; s += step) sell_slice<T, V, Epi, Gather>(A, x, epi, slice_at(A, s));
 }
 
 // Software-pipelined SELL (variant bits 2048 | 8; matrices whose slices are
@@ -1047,7 +1056,7 @@ template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell2(const CsrArgs &A, const Gather &x, Epi &epi) {
   int s, step, end;
   sell_range((int)A.nsl, s, step, end);
-  for (; s < end; s += step) sell_slice2<T, V, Epi, Gather>(A, x, epi, s);
+  for (; s < end; s += step) sell_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, s));
 }
 
 // LDS layout of a variant's kernel
@@ -1576,7 +1585,8 @@ inline int elem_grid(int64_t n, int per_thread) {
 }
 
 inline CsrArgs args(const CsrDev &A) {
-  return CsrArgs{A.rowptr, A.col, A.rb, A.rbk, A.nrb, A.n, A.sl, A.sdict, A.sidx, A.sval, A.nsl};
+  return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
+                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder};
 }
 
 }  // namespace

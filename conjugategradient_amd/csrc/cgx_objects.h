@@ -89,6 +89,7 @@ struct cgx_csr {
   // SELL-64 copy (cgx::CsrDev::sl ...), null when absent
   void *d_sell_sl = nullptr, *d_sell_dict = nullptr, *d_sell_idx = nullptr;
   void *d_sell_val = nullptr;
+  void *d_sell_order = nullptr;
   int64_t sell_padded = 0;
 };
 

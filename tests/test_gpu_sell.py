@@ -52,6 +52,8 @@ def _matrix_cases(oracle):
     return {
         "poisson2d": oracle.poisson(2, 96, 80, 1),
         "poisson3d_ragged": oracle.poisson(3, 23, 19, 17),     # n % 64 != 0
+        # planes of 33,280 rows (> 256 slices): the host builds a visit order
+        "poisson3d_wide": oracle.poisson(3, 256, 130, 3),
         "banded": banded(10_007, half=9),
         "empty_rows": banded(3_001, half=6, empty_every=13),
         "tiny": (np.array([0, 1, 3, 4], np.int32), np.array([0, 0, 1, 2], np.int32),
@@ -67,10 +69,12 @@ def _sell_info(m):
 
 
 @pytest.mark.parametrize("R", [1, 2])
-@pytest.mark.parametrize("case", ["poisson2d", "poisson3d_ragged", "banded", "empty_rows",
-                                  "tiny"])
+@pytest.mark.parametrize("case", ["poisson2d", "poisson3d_ragged", "poisson3d_wide", "banded",
+                                  "empty_rows", "tiny"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype, R):
+def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype, R, monkeypatch):
+    if case == "poisson3d_wide":
+        monkeypatch.setenv("CGX_SELL_ORDER", "1")   # the opt-in visit order
     rp, cl, vl = _matrix_cases(oracle)[case]
     n = len(rp) - 1
     A = Matrix(queue, vl, cl, rp, dtype=dtype)
@@ -153,10 +157,12 @@ def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle, R):
 
 
 @pytest.mark.parametrize("sell", ["1", "2", "0"])
-@pytest.mark.parametrize("dim,n", [(2, 64), (3, 20)])
+@pytest.mark.parametrize("dim,n", [(2, 64), (3, 20), (3, 0)])
 def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     monkeypatch.setenv("CGX_SELL", sell)
-    rp, cl, vl = oracle.poisson(dim, n, n, n)
+    monkeypatch.setenv("CGX_SELL_ORDER", "1")
+    # n = 0: 256 x 130 x 3, wide planes (the visit-order path)
+    rp, cl, vl = oracle.poisson(dim, n, n, n) if n else oracle.poisson(3, 256, 130, 3)
     b = np.arange(1, len(rp), dtype=np.float64)
     cg = cga.CG.createCG()
     cg.setMatrix(vl, cl, rp)
