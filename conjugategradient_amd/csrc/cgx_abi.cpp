@@ -158,13 +158,27 @@ template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   if (A->dist && A->halo.n_ghost + A->halo.send_total > 0) {
     if ((rc = dist_halo_exchange(A, p, s))) return rc;
   }
+  // The dots travel as per-workgroup partials summed by the next kernel
+  // (single device). A partitioned run finalizes each local dot into the
+  // scalar ring, all-reduces it, and the next kernel reads the ring.
+  const int npp = Launch<T>::spmv_parts(A->dev), npr = Launch<T>::update_parts(cg->n);
   if ((rc = timed(cg, 1, s, [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s); })))
     return rc;
-  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
-  if ((rc = timed(cg, 2, s, [&] { return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s); })))
+  if (A->dist) {
+    CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
+    if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
+  }
+  if ((rc = timed(cg, 2, s, [&] {
+         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp);
+       })))
     return rc;
-  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
-  if ((rc = timed(cg, 3, s, [&] { return Launch<T>::update_xp(cg->n, x, p, r, st, slot, s); })))
+  if (A->dist) {
+    CGX_HIP(Launch<T>::finalize(ws->rr_part, npr, &st->rr[slot], s));
+    if ((rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
+  }
+  if ((rc = timed(cg, 3, s, [&] {
+         return Launch<T>::update_xp(cg->n, x, p, r, st, slot, ws, A->dist ? 0 : npr, s);
+       })))
     return rc;
   return CGX_OK;
 }
@@ -184,14 +198,24 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   if (A->dist && A->halo.n_ghost + A->halo.send_total > 0) {
     if ((rc = dist_halo_exchange(A, p, s))) return rc;
   }
+  const int npp = Launch<T>::spmv_parts(A->dev), npr = Launch<T>::update_parts(cg->n);
   if ((rc = timed(cg, 1, s, [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s); })))
     return rc;
-  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
-  if ((rc = timed(cg, 2, s, [&] { return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s); })))
+  if (A->dist) {
+    CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
+    if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
+  }
+  if ((rc = timed(cg, 2, s, [&] {
+         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp);
+       })))
     return rc;
-  if (A->dist && (rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
+  if (A->dist) {
+    CGX_HIP(Launch<T>::finalize(ws->rr_part, npr, &st->rr[slot], s));
+    if ((rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
+  }
   if ((rc = timed(cg, 3, s, [&] {
-         return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, s);
+         return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, A->dist ? 0 : npr,
+                                          s);
        })))
     return rc;
   return CGX_OK;

@@ -59,6 +59,10 @@ template <typename T> struct RedWs {
   unsigned int pad[7];
   T gsum[kMaxRed * kRedGroups];
   T partials[kMaxRed * kMaxGrid];
+  // per-workgroup partials of the iteration's two dots, summed by the NEXT
+  // kernel (every workgroup, fixed order): no tail chain in the producer
+  T pap_part[kMaxGrid];
+  T rr_part[kMaxGrid];
 };
 
 // SELL copy of a matrix (built by cgx_csr_create when the matrix qualifies,
@@ -114,16 +118,24 @@ template <typename T> struct Launch {
                              int slot, RedWs<T> *ws, hipStream_t s);
   static hipError_t spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                      CgScalars<T> *st, RedWs<T> *ws, hipStream_t s);
+  // np_pap > 0: p.Ap from the spmv_dot partials; 0: from st->pAp[slot]
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                             RedWs<T> *ws, hipStream_t s, bool fused = false);
+                             RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0);
+  // partial counts the consumers pass (the producers' grid sizes)
+  static int spmv_parts(const CsrDev &A);
+  static int update_parts(int64_t n);
+  // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
+  static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);
   static hipError_t spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
                                CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s);
   static hipError_t flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,
                             RedWs<T> *ws, hipStream_t s);
+  // np_rr > 0: r.r from the update_r partials; 0: from st->rr[slot]
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                              int slot, hipStream_t s);
+                              int slot, RedWs<T> *ws, int np_rr, hipStream_t s);
   static hipError_t update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
-                                   const T *r, CgScalars<T> *st, int slot, hipStream_t s);
+                                   const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                   int np_rr, hipStream_t s);
   static hipError_t flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                 hipStream_t s);
   static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,

@@ -87,6 +87,21 @@ __device__ __forceinline__ void block_sum(T (&v)[K], T *lds) {
   __syncthreads();
 }
 
+// Sum of the previous kernel's per-workgroup partials, in the same fixed
+// order in every workgroup (thread t: t, t + 256, ...; then block_sum), so
+// all workgroups get the identical value. Stream order makes the producer's
+// plain stores visible; no atomics, no write-through. Uniform control flow.
+template <typename T>
+__device__ __forceinline__ T sum_parts(const T *__restrict__ part, int np, T *lds) {
+  __shared__ T bc;
+  T v[1] = {T(0)};
+  for (int i = threadIdx.x; i < np; i += kBlock) v[0] += part[i];
+  block_sum<T, 1>(v, lds);
+  if (threadIdx.x == 0) bc = v[0];
+  __syncthreads();
+  return bc;
+}
+
 // Grid-wide deterministic reduction. Every workgroup publishes its block sum
 // write-through and takes the ticket of its group (blockIdx % kRedGroups). The
 // last arrival of a group sums the group's partials in workgroup order and
@@ -1254,8 +1269,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restr
   __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
+  // this workgroup's share of p.Ap; k_update_r sums the partials
   T v[1] = {e.acc};
-  if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) st->pAp[slot] = v[0];
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[blockIdx.x] = v[0];
 }
 
 // Fused iteration, kernel 1 of 2 (slot s of body k). Reads active[s] (run
@@ -1339,15 +1356,19 @@ template <typename T, bool FUSED>
 __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
-                                                     RedWs<T> *ws) {
+                                                     RedWs<T> *ws, int np_pap) {
   if (!st->active[slot]) {
     if (FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
     return;
   }
   __shared__ T red[4];
   __shared__ int flag;
-  const T alpha = st->rxr[slot] / st->pAp[slot];
-  if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // for the deferred x update
+  // p.Ap: the spmv_dot partials (single device) or st (fused mode, or
+  // partitioned runs after the all-reduce)
+  const T pAp = (!FUSED && np_pap > 0) ? sum_parts(ws->pap_part, np_pap, red) : st->pAp[slot];
+  const T alpha = st->rxr[slot] / pAp;
+  if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // the record; the deferred x update
+    st->pAp[slot] = pAp;
     st->alpha[slot] = alpha;
     st->skip[slot] = 0;
   }
@@ -1386,6 +1407,11 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
     acc += v * v;
   }
   T v[1] = {acc};
+  if constexpr (!FUSED) {  // this workgroup's share of r.r; the next kernel sums them
+    block_sum<T, 1>(v, red);
+    if (threadIdx.x == 0) ws->rr_part[blockIdx.x] = v[0];
+    return;
+  }
   if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) {
     st->rr[slot] = v[0];
     if (FUSED) {
@@ -1408,15 +1434,17 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__ x,
                                                       T *__restrict__ p,
                                                       const T *__restrict__ r,
-                                                      CgScalars<T> *st, int slot) {
+                                                      CgScalars<T> *st, int slot,
+                                                      RedWs<T> *ws, int np_rr) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
   }
+  __shared__ T red[4];
   const T rxr = st->rxr[slot];
   const T alpha = rxr / st->pAp[slot];
-  const T rr = st->rr[slot];
+  const T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
   const T beta = rr / rxr;
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
@@ -1459,6 +1487,7 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
       x[n - 1] = x[n - 1] + alpha * pv;
       p[n - 1] = r[n - 1] + beta * pv;
     }
+    if (np_rr > 0) st->rr[slot] = rr;  // the record
     const long long m = st->bodies + 1;
     st->bodies = m;
     const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
@@ -1628,14 +1657,16 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
                                                            const T *p, T *pn, const T *P0,
                                                            const T *P1, const T *P2,
                                                            const T *__restrict__ r,
-                                                           CgScalars<T> *st, int slot) {
+                                                           CgScalars<T> *st, int slot,
+                                                           RedWs<T> *ws, int np_rr) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
   }
+  __shared__ T red[4];
   const T rxr = st->rxr[slot];
-  const T rr = st->rr[slot];
+  const T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
   const T beta = rr / rxr;
   // slot-3 flush: alphas and skips of the group, written by earlier launches
   T a[4] = {T(0), T(0), T(0), T(0)};
@@ -1703,6 +1734,7 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
       pn[n - 1] = r[n - 1] + beta * pv;
     }
     // stop rule, as k_update_xp
+    if (np_rr > 0) st->rr[slot] = rr;  // the record
     const long long m = st->bodies + 1;
     st->bodies = m;
     const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
@@ -1747,6 +1779,15 @@ __global__ __launch_bounds__(kBlock) void k_flush_defer(int64_t n, T *__restrict
       if (use[t]) xv = xv + a[t] * Ps[t][i];
     x[i] = xv;
   }
+}
+
+// *dst = sum of part[0..np) in sum_parts order (partitioned runs: the local
+// dot before its RCCL all-reduce)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_finalize(const T *__restrict__ part, int np, T *dst) {
+  __shared__ T red[4];
+  const T v = sum_parts(part, np, red);
+  if (threadIdx.x == 0) *dst = v;
 }
 
 template <typename T> __global__ void k_mark_defer(CgScalars<T> *st) {
@@ -1886,15 +1927,21 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
 }
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                               RedWs<T> *ws, hipStream_t s, bool fused) {
+                               RedWs<T> *ws, hipStream_t s, bool fused, int np_pap) {
   if (fused) {
     hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws);
+                       st, slot, ws, 0);
   } else {
     hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws);
+                       st, slot, ws, np_pap);
   }
   return hipGetLastError();
+}
+template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) { return grid_rows(A.nrb); }
+template <typename T> int Launch<T>::update_parts(int64_t n) { return grid_elems(n); }
+template <typename T>
+hipError_t Launch<T>::finalize(const T *part, int np, T *dst, hipStream_t s) {
+  CGX_LAUNCH(k_finalize<T>, 1, part, np, dst);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
@@ -1909,18 +1956,19 @@ hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int
 }
 template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                                int slot, hipStream_t s) {
-  CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot);
+                                int slot, RedWs<T> *ws, int np_rr, hipStream_t s) {
+  CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot, ws, np_rr);
 }
 template <typename T>
 hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
-                                     const T *r, CgScalars<T> *st, int slot, hipStream_t s) {
+                                     const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                     int np_rr, hipStream_t s) {
   if (slot == 3) {
     CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n), n, x, p, pn, (const T *)P[0],
-               (const T *)P[1], (const T *)P[2], r, st, slot);
+               (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr);
   }
   CGX_LAUNCH((k_update_p_defer<T, false>), grid_elems(n), n, x, p, pn, (const T *)P[0],
-             (const T *)P[1], (const T *)P[2], r, st, slot);
+             (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr);
 }
 template <typename T>
 hipError_t Launch<T>::flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
