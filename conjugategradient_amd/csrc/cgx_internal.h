@@ -114,13 +114,15 @@ template <typename T> struct Launch {
   static hipError_t cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                             CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
                             hipStream_t s);
+  // rev: sweep the rows high to low (alternating sweep directions, cgx_abi.cpp)
   static hipError_t spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
-                             int slot, RedWs<T> *ws, hipStream_t s);
+                             int slot, RedWs<T> *ws, hipStream_t s, int rev = 0);
   static hipError_t spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                      CgScalars<T> *st, RedWs<T> *ws, hipStream_t s);
   // np_pap > 0: p.Ap from the spmv_dot partials; 0: from st->pAp[slot]
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                             RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0);
+                             RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0,
+                             int rev = 0);
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
   static int update_parts(int64_t n);
@@ -132,10 +134,10 @@ template <typename T> struct Launch {
                             RedWs<T> *ws, hipStream_t s);
   // np_rr > 0: r.r from the update_r partials; 0: from st->rr[slot]
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                              int slot, RedWs<T> *ws, int np_rr, hipStream_t s);
+                              int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev = 0);
   static hipError_t update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
                                    const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
-                                   int np_rr, hipStream_t s);
+                                   int np_rr, hipStream_t s, int rev = 0);
   static hipError_t flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                 hipStream_t s);
   static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,

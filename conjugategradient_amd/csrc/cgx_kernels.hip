@@ -211,6 +211,7 @@ struct CsrArgs {
   const void *sval;
   int64_t nsl;
   const int *__restrict__ sorder;
+  int rev;  // per launch: walk the rows high to low (alternating sweeps)
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -863,15 +864,18 @@ template <typename T> struct SellLds {
 // The waves of one XCD walk a contiguous slice range (as variant bit 1);
 // consecutive slices on the waves of one workgroup. Slice indices fit int
 // (n < 2^31), which keeps the loop control on the scalar unit.
-__device__ __forceinline__ void sell_range(int nsl, int &first, int &step, int &end) {
+__device__ __forceinline__ void sell_range(int nsl, int &first, int &step, int &end,
+                                           int &lo) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = gridDim.x;
   if ((G & 7) == 0) {
     const int g = blockIdx.x & 7;
-    first = (int)(((int64_t)nsl * g) >> 3) + (blockIdx.x >> 3) * 4 + wid;
+    lo = (int)(((int64_t)nsl * g) >> 3);
+    first = lo + (blockIdx.x >> 3) * 4 + wid;
     end = (int)(((int64_t)nsl * (g + 1)) >> 3);
     step = (G >> 3) * 4;
   } else {
+    lo = 0;
     first = blockIdx.x * 4 + wid;
     end = nsl;
     step = G * 4;
@@ -929,9 +933,10 @@ __device__ __forceinline__ int slice_at(const CsrArgs &A, int k) {
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell(const CsrArgs &A, const Gather &x, Epi &epi) {
-  int s, step, end;
-  sell_range((int)A.nsl, s, step, end);
-  for (; s < end; s += step) sell_slice<T, V, Epi, Gather>(A, x, epi, slice_at(A, s));
+  int s, step, end, lo;
+  sell_range((int)A.nsl, s, step, end, lo);
+  for (; s < end; s += step)
+    sell_slice<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
 
 // Software-pipelined SELL (variant bits 2048 | 8; matrices whose slices are
@@ -946,8 +951,8 @@ __device__ __forceinline__ void spmv_sell_pipe(const CsrArgs &A, const Gather &x
   constexpr bool NT = (V & 2) != 0;
   const T *__restrict__ sval = static_cast<const T *>(A.sval);
   const int lane = threadIdx.x & 63;
-  int first, step, end;
-  sell_range((int)A.nsl, first, step, end);
+  int first, step, end, lo;
+  sell_range((int)A.nsl, first, step, end, lo);
   const int full = (int)(A.n / kSellRows);  // slices whose 64 rows all exist
   const int pend = min(end, full);
   auto issue = [&](int q, unsigned long long &iw, T(&v)[8], int &dv) {
@@ -1069,9 +1074,10 @@ __device__ __forceinline__ void sell_slice2(const CsrArgs &A, const Gather &x, E
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell2(const CsrArgs &A, const Gather &x, Epi &epi) {
-  int s, step, end;
-  sell_range((int)A.nsl, s, step, end);
-  for (; s < end; s += step) sell_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, s));
+  int s, step, end, lo;
+  sell_range((int)A.nsl, s, step, end, lo);
+  for (; s < end; s += step)
+    sell_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
 
 // LDS layout of a variant's kernel
@@ -1265,7 +1271,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restr
                                                      const T *__restrict__ p,
                                                      T *__restrict__ Ap, CgScalars<T> *st,
                                                      int slot, RedWs<T> *ws) {
-  if (!st->active[slot]) return;
+  if (!st->active[slot]) return;  // (A.rev: the launcher's sweep direction)
   __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
@@ -1356,7 +1362,7 @@ template <typename T, bool FUSED>
 __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
-                                                     RedWs<T> *ws, int np_pap) {
+                                                     RedWs<T> *ws, int np_pap, int rev) {
   if (!st->active[slot]) {
     if (FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
     return;
@@ -1378,26 +1384,30 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
   V *r2 = reinterpret_cast<V *>(r);
   const V *a2 = reinterpret_cast<const V *>(Ap);
   T acc = T(0);
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
     V rv[4], av[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) { rv[u] = r2[i + u * stride]; av[u] = a2[i + u * stride]; }
+    for (int u = 0; u < 4; ++u) {
+      rv[u] = r2[E(i + u * stride)];
+      av[u] = a2[E(i + u * stride)];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       rv[u].x = rv[u].x - alpha * av[u].x;
       rv[u].y = rv[u].y - alpha * av[u].y;
-      r2[i + u * stride] = rv[u];
+      r2[E(i + u * stride)] = rv[u];
       acc += rv[u].x * rv[u].x;
       acc += rv[u].y * rv[u].y;
     }
   }
   for (; i < n2; i += stride) {
-    V rv = r2[i];
-    const V av = a2[i];
+    V rv = r2[E(i)];
+    const V av = a2[E(i)];
     rv.x = rv.x - alpha * av.x;
     rv.y = rv.y - alpha * av.y;
-    r2[i] = rv;
+    r2[E(i)] = rv;
     acc += rv.x * rv.x;
     acc += rv.y * rv.y;
   }
@@ -1435,7 +1445,7 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
                                                       T *__restrict__ p,
                                                       const T *__restrict__ r,
                                                       CgScalars<T> *st, int slot,
-                                                      RedWs<T> *ws, int np_rr) {
+                                                      RedWs<T> *ws, int np_rr, int rev) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
@@ -1452,14 +1462,15 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
   V *x2 = reinterpret_cast<V *>(x);
   V *p2 = reinterpret_cast<V *>(p);
   const V *rv2 = reinterpret_cast<const V *>(r);
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
     V xv[4], pv[4], rv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      xv[u] = x2[i + u * stride];
-      pv[u] = p2[i + u * stride];
-      rv[u] = rv2[i + u * stride];
+      xv[u] = x2[E(i + u * stride)];
+      pv[u] = p2[E(i + u * stride)];
+      rv[u] = rv2[E(i + u * stride)];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1467,19 +1478,19 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
       xv[u].y = xv[u].y + alpha * pv[u].y;
       pv[u].x = rv[u].x + beta * pv[u].x;
       pv[u].y = rv[u].y + beta * pv[u].y;
-      x2[i + u * stride] = xv[u];
-      p2[i + u * stride] = pv[u];
+      x2[E(i + u * stride)] = xv[u];
+      p2[E(i + u * stride)] = pv[u];
     }
   }
   for (; i < n2; i += stride) {
-    V xv = x2[i], pv = p2[i];
-    const V rv = rv2[i];
+    V xv = x2[E(i)], pv = p2[E(i)];
+    const V rv = rv2[E(i)];
     xv.x = xv.x + alpha * pv.x;
     xv.y = xv.y + alpha * pv.y;
     pv.x = rv.x + beta * pv.x;
     pv.y = rv.y + beta * pv.y;
-    x2[i] = xv;
-    p2[i] = pv;
+    x2[E(i)] = xv;
+    p2[E(i)] = pv;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (n & 1) {
@@ -1615,7 +1626,7 @@ inline int elem_grid(int64_t n, int per_thread) {
 
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
-                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder};
+                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0};
 }
 
 }  // namespace
@@ -1658,7 +1669,7 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
                                                            const T *P1, const T *P2,
                                                            const T *__restrict__ r,
                                                            CgScalars<T> *st, int slot,
-                                                           RedWs<T> *ws, int np_rr) {
+                                                           RedWs<T> *ws, int np_rr, int rev) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
@@ -1715,12 +1726,13 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
     }
     pn2[i] = o;
   };
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   for (; i + 3 * stride < n2; i += 4 * stride) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) body(i + u * stride);
+    for (int u = 0; u < 4; ++u) body(E(i + u * stride));
   }
-  for (; i < n2; i += stride) body(i);
+  for (; i < n2; i += stride) body(E(i));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (n & 1) {
       const T pv = p[n - 1];
@@ -1903,9 +1915,10 @@ hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
-                               int slot, RedWs<T> *ws, hipStream_t s) {
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, slot,
-                  ws);
+                               int slot, RedWs<T> *ws, hipStream_t s, int rev) {
+  CsrArgs a = args(A);
+  a.rev = rev;
+  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
@@ -1927,13 +1940,13 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
 }
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                               RedWs<T> *ws, hipStream_t s, bool fused, int np_pap) {
+                               RedWs<T> *ws, hipStream_t s, bool fused, int np_pap, int rev) {
   if (fused) {
     hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws, 0);
+                       st, slot, ws, 0, 0);
   } else {
     hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws, np_pap);
+                       st, slot, ws, np_pap, rev);
   }
   return hipGetLastError();
 }
@@ -1956,19 +1969,19 @@ hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int
 }
 template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                                int slot, RedWs<T> *ws, int np_rr, hipStream_t s) {
-  CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot, ws, np_rr);
+                                int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev) {
+  CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot, ws, np_rr, rev);
 }
 template <typename T>
 hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
                                      const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
-                                     int np_rr, hipStream_t s) {
+                                     int np_rr, hipStream_t s, int rev) {
   if (slot == 3) {
     CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n), n, x, p, pn, (const T *)P[0],
-               (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr);
+               (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev);
   }
   CGX_LAUNCH((k_update_p_defer<T, false>), grid_elems(n), n, x, p, pn, (const T *)P[0],
-             (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr);
+             (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev);
 }
 template <typename T>
 hipError_t Launch<T>::flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
