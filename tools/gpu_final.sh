@@ -22,3 +22,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $C ok"
 done
 find $OUT -name "*stats*.csv" | head
+timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 2 --grid 64 --transport host --no-cpu > $OUT/bench_2rank_host.log 2>&1 || { echo DIST_BENCH_FAIL; tail -20 $OUT/bench_2rank_host.log; exit 1; }
+grep metric $OUT/bench_2rank_host.log | cut -c1-300
+timeout -k 10 600 python tools/configs_bench.py > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; tail -20 $OUT/configs.log; exit 1; }
+grep config $OUT/configs.log
