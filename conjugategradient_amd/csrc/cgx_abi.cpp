@@ -148,6 +148,45 @@ int harvest_events(cgx_cg *cg, int64_t active_iters) {
   return CGX_OK;
 }
 
+// SpMV + p.Ap of body `slot` on p, with the halo exchange of a partitioned
+// matrix: a SELL matrix split into interior and boundary slices runs the
+// interior ones while the exchange is in flight (RCCL on the comm stream),
+// then the boundary ones; otherwise exchange, then one SpMV. *np: partials.
+template <typename T>
+int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
+  cgx_csr *A = cg->A;
+  hipStream_t s = cg->ctx->stream;
+  auto *st = (CgScalars<T> *)cg->st;
+  auto *ws = (RedWs<T> *)cg->ws;
+  T *Ap = (T *)cg->Ap;
+  int rc;
+  const bool halo = A->dist && A->halo.n_ghost + A->halo.send_total > 0;
+  if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & 2048)) {
+    bool async = false;
+    if ((rc = dist_halo_post(A, p, s, &async))) return rc;
+    const int gi = Launch<T>::slice_grid(A->split_ni);
+    if ((rc = timed(cg, 1, s, [&] {
+           return Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
+                                             ws, s, rev);
+         })))
+      return rc;
+    if (async && (rc = dist_halo_wait(A, s))) return rc;
+    if ((rc = timed(cg, 1, s, [&] {
+           return Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb, gi, p,
+                                             Ap, st, slot, ws, s, rev);
+         })))
+      return rc;
+    *np = gi + Launch<T>::slice_grid(A->split_nb);
+    return CGX_OK;
+  }
+  if (halo && (rc = dist_halo_exchange(A, p, s))) return rc;
+  if ((rc = timed(cg, 1, s,
+                  [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s, rev); })))
+    return rc;
+  *np = Launch<T>::spmv_parts(A->dev);
+  return CGX_OK;
+}
+
 template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   cgx_csr *A = cg->A;
   hipStream_t s = cg->ctx->stream;
@@ -155,18 +194,14 @@ template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   auto *ws = (RedWs<T> *)cg->ws;
   T *p = (T *)cg->p, *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
   int rc;
-  if (A->dist && A->halo.n_ghost + A->halo.send_total > 0) {
-    if ((rc = dist_halo_exchange(A, p, s))) return rc;
-  }
   // The dots travel as per-workgroup partials summed by the next kernel
   // (single device). A partitioned run finalizes each local dot into the
   // scalar ring, all-reduces it, and the next kernel reads the ring.
-  const int npp = Launch<T>::spmv_parts(A->dev), npr = Launch<T>::update_parts(cg->n);
+  const int npr = Launch<T>::update_parts(cg->n);
   // sweep directions: each kernel starts where the previous one ended
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
-  if ((rc = timed(cg, 1, s,
-                  [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s, par); })))
-    return rc;
+  int npp = 0;
+  if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
   if (A->dist) {
     CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
     if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
@@ -199,15 +234,11 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   T *p = P[slot], *pn = P[(slot + 1) & 3];
   T *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
   int rc;
-  if (A->dist && A->halo.n_ghost + A->halo.send_total > 0) {
-    if ((rc = dist_halo_exchange(A, p, s))) return rc;
-  }
-  const int npp = Launch<T>::spmv_parts(A->dev), npr = Launch<T>::update_parts(cg->n);
+  const int npr = Launch<T>::update_parts(cg->n);
   // sweep directions: each kernel starts where the previous one ended
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
-  if ((rc = timed(cg, 1, s,
-                  [&] { return Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s, par); })))
-    return rc;
+  int npp = 0;
+  if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
   if (A->dist) {
     CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
     if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
@@ -662,7 +693,7 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 
 void free_sell(cgx_csr *A) {
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
-                   &A->d_sell_order}) {
+                   &A->d_sell_order, (void **)&A->d_split}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -672,6 +703,7 @@ void free_sell(cgx_csr *A) {
   A->dev.sval = nullptr;
   A->dev.nsl = 0;
   A->dev.sorder = nullptr;
+  A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
   A->sell_padded = 0;

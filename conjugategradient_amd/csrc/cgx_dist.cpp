@@ -170,6 +170,47 @@ int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
   return CGX_OK;
 }
 
+int dist_halo_post(cgx_csr *A, void *vec_ext, hipStream_t s, bool *async) {
+  *async = false;
+  cgx_ctx *ctx = A->ctx;
+  Halo &h = A->halo;
+  if (!A->dist || !multi(ctx) || (h.n_ghost == 0 && h.send_total == 0)) return CGX_OK;
+  if (ctx->host || !ctx->cstream || !A->ev_pack || !A->ev_halo)
+    return dist_halo_exchange(A, vec_ext, s);  // synchronous
+  const size_t es = dtype_size(A->dtype);
+  if (h.send_total > 0) {
+    if (A->dtype == CGX_F32)
+      CGX_HIP(Launch<float>::gather((const float *)vec_ext, h.d_send_idx, h.send_total,
+                                    (float *)h.d_send_buf, s));
+    else
+      CGX_HIP(Launch<double>::gather((const double *)vec_ext, h.d_send_idx, h.send_total,
+                                     (double *)h.d_send_buf, s));
+  }
+  // the exchange runs on the comm stream once the pack (and everything before
+  // it on s) is done; the interior rows proceed on s meanwhile
+  CGX_HIP(hipEventRecord(A->ev_pack, s));
+  CGX_HIP(hipStreamWaitEvent(ctx->cstream, A->ev_pack, 0));
+  const ncclDataType_t t = nccl_type(A->dtype);
+  CGX_NCCL(ncclGroupStart());
+  for (size_t i = 0; i < h.nbr.size(); ++i) {
+    if (h.send_cnt[i] > 0)
+      CGX_NCCL(ncclSend((char *)h.d_send_buf + (size_t)h.send_off[i] * es,
+                        (size_t)h.send_cnt[i], t, h.nbr[i], ctx->comm, ctx->cstream));
+    if (h.recv_cnt[i] > 0)
+      CGX_NCCL(ncclRecv((char *)vec_ext + (size_t)(A->dev.n + h.recv_off[i]) * es,
+                        (size_t)h.recv_cnt[i], t, h.nbr[i], ctx->comm, ctx->cstream));
+  }
+  CGX_NCCL(ncclGroupEnd());
+  CGX_HIP(hipEventRecord(A->ev_halo, ctx->cstream));
+  *async = true;
+  return CGX_OK;
+}
+
+int dist_halo_wait(cgx_csr *A, hipStream_t s) {
+  CGX_HIP(hipStreamWaitEvent(s, A->ev_halo, 0));
+  return CGX_OK;
+}
+
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s) {
   if (!multi(ctx)) return CGX_OK;
   if (ctx->host) {
@@ -195,6 +236,9 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
 }
 
 int dist_destroy_halo(cgx_csr *A) {
+  if (A->ev_pack) (void)hipEventDestroy(A->ev_pack);
+  if (A->ev_halo) (void)hipEventDestroy(A->ev_halo);
+  A->ev_pack = A->ev_halo = nullptr;
   if (A->halo.d_send_idx) (void)hipFree(A->halo.d_send_idx);
   if (A->halo.d_send_buf) (void)hipFree(A->halo.d_send_buf);
   if (A->halo.h_send) (void)hipHostFree(A->halo.h_send);
@@ -206,6 +250,11 @@ int dist_destroy_halo(cgx_csr *A) {
 }
 
 int dist_comm_destroy(cgx_ctx *ctx) {
+  if (ctx->cstream) {
+    (void)hipStreamSynchronize(ctx->cstream);
+    (void)hipStreamDestroy(ctx->cstream);
+    ctx->cstream = nullptr;
+  }
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   ctx->comm = nullptr;
   delete ctx->host;
@@ -311,6 +360,7 @@ extern "C" int cgx_dist_init(cgx_ctx *ctx, int rank, int world, const char *id, 
   ncclComm_t comm = nullptr;
   CGX_NCCL(ncclCommInitRank(&comm, world, uid, rank));
   ctx->comm = comm;
+  if (world > 1) CGX_HIP(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
   ctx->rank = rank;
   ctx->world = world;
   return CGX_OK;
@@ -479,7 +529,44 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     cgx_csr_destroy(A);
     return rc;
   }
+  // interior / boundary slices of the SELL copy: the halo exchange overlaps
+  // the interior ones (enqueue_iter); a slab of a stencil has one boundary
+  // plane per neighbour
+  if (A->dev.sl && h.n_ghost > 0) {
+    const int64_t H = (int64_t)kSellRows * A->dev.sell_r, nsl = A->dev.nsl;
+    std::vector<int> in, bd;
+    for (int64_t q = 0; q < nsl; ++q) {
+      const int64_t r0 = q * H, r1 = std::min<int64_t>(n_local, r0 + H);
+      bool ghost = false;
+      for (int64_t k = hrp[(size_t)r0]; k < hrp[(size_t)r1] && !ghost; ++k)
+        ghost = hcol[(size_t)k] >= n_local;
+      (ghost ? bd : in).push_back((int)q);
+    }
+    if (!in.empty() && !bd.empty()) {
+      in.insert(in.end(), bd.begin(), bd.end());
+      e = hipMalloc(&A->d_split, in.size() * sizeof(int));
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(A->d_split, in.data(), in.size() * sizeof(int), hipMemcpyHostToDevice,
+                           s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess && ctx->cstream) e = hipEventCreateWithFlags(&A->ev_pack, hipEventDisableTiming);
+      if (e == hipSuccess && ctx->cstream) e = hipEventCreateWithFlags(&A->ev_halo, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        cgx_csr_destroy(A);
+        return hip_fail(e, "cgx_csr_create_dist(slice split)");
+      }
+      A->split_ni = (int)(in.size() - bd.size());
+      A->split_nb = (int)bd.size();
+    }
+  }
   *out = A;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_split_info(cgx_csr *A, int *ni, int *nb) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  if (ni) *ni = A->split_ni;
+  if (nb) *nb = A->split_nb;
   return CGX_OK;
 }
 

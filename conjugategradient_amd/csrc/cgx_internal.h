@@ -61,7 +61,7 @@ template <typename T> struct RedWs {
   T partials[kMaxRed * kMaxGrid];
   // per-workgroup partials of the iteration's two dots, summed by the NEXT
   // kernel (every workgroup, fixed order): no tail chain in the producer
-  T pap_part[kMaxGrid];
+  T pap_part[2 * kMaxGrid];  // room for the interior + boundary launches of a split SpMV
   T rr_part[kMaxGrid];
 };
 
@@ -125,6 +125,12 @@ template <typename T> struct Launch {
                              int rev = 0);
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
+  // SpMV + p.Ap over `count` SELL slices listed at `list` (device), partials
+  // at [part_off, part_off + slice_grid(count)); SELL matrices only
+  static hipError_t spmv_dot_slices(const CsrDev &A, const int *list, int count, int part_off,
+                                    const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                    hipStream_t s, int rev = 0);
+  static int slice_grid(int count);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);

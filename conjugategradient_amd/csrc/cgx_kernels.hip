@@ -211,7 +211,8 @@ struct CsrArgs {
   const void *sval;
   int64_t nsl;
   const int *__restrict__ sorder;
-  int rev;  // per launch: walk the rows high to low (alternating sweeps)
+  int rev;       // per launch: walk the rows high to low (alternating sweeps)
+  int part_off;  // per launch: first partial slot of k_spmv_dot (split launches)
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -1278,7 +1279,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restr
   // this workgroup's share of p.Ap; k_update_r sums the partials
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[blockIdx.x] = v[0];
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
 }
 
 // Fused iteration, kernel 1 of 2 (slot s of body k). Reads active[s] (run
@@ -1626,7 +1627,7 @@ inline int elem_grid(int64_t n, int per_thread) {
 
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
-                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0};
+                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0};
 }
 
 }  // namespace
@@ -1850,7 +1851,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 
 #define CGX_LAUNCH_V(KERNEL, VV, ...)                                          \
   do {                                                                         \
-    hipLaunchKernelGGL((KERNEL<T, VV>), dim3(grid_rows(A.nrb)), dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((KERNEL<T, VV>), dim3(spmv_grid_), dim3(kBlock), 0, s,   \
                        __VA_ARGS__);                                           \
     return hipGetLastError();                                                  \
   } while (0)
@@ -1904,12 +1905,14 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 
 template <typename T>
 hipError_t Launch<T>::spmv(const CsrDev &A, const T *x, T *y, hipStream_t s) {
+  const int spmv_grid_ = grid_rows(A.nrb);
   CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv, args(A), (const T *)A.val, x, y);
 }
 template <typename T>
 hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                               CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
                               hipStream_t s) {
+  const int spmv_grid_ = grid_rows(A.nrb);
   CGX_SPMV_SWITCH(spmv_variant<T>(A), k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws,
                   tol, cap);
 }
@@ -1918,12 +1921,34 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
                                int slot, RedWs<T> *ws, hipStream_t s, int rev) {
   CsrArgs a = args(A);
   a.rev = rev;
+  const int spmv_grid_ = grid_rows(A.nrb);
   CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
+}
+// SpMV + p.Ap over a list of SELL slices (a partitioned matrix's interior or
+// boundary slices), its partials at [part_off, part_off + grid)
+template <typename T>
+hipError_t Launch<T>::spmv_dot_slices(const CsrDev &A, const int *list, int count, int part_off,
+                                      const T *p, T *Ap, CgScalars<T> *st, int slot,
+                                      RedWs<T> *ws, hipStream_t s, int rev) {
+  const int v = spmv_variant<T>(A);
+  if (!(v & 2048) || count < 1) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.sorder = list;
+  a.nsl = count;
+  a.part_off = part_off;
+  a.rev = rev;
+  const int spmv_grid_ = slice_grid(count);
+  CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
+}
+template <typename T> int Launch<T>::slice_grid(int count) {
+  const int g = (count + 3) / 4;  // one wave per slice, 4 waves per workgroup
+  return g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                        CgScalars<T> *st, RedWs<T> *ws, hipStream_t s) {
   const int vv = spmv_variant<T>(A, v);
+  const int spmv_grid_ = grid_rows(A.nrb);
   switch (vv) {  // timing ablations (bits 16/32) exist for this kernel only
     case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -1959,6 +1984,7 @@ hipError_t Launch<T>::finalize(const T *part, int np, T *dst, hipStream_t s) {
 template <typename T>
 hipError_t Launch<T>::spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
                                  CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s) {
+  const int spmv_grid_ = grid_rows(A.nrb);
   CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_fused, args(A), (const T *)A.val, r, pp, pc, x, Ap,
                   st, slot, ws);
 }
@@ -2019,6 +2045,7 @@ hipError_t Launch<T>::iota(T *d, int64_t n, double offset, hipStream_t s) {
 template <typename T>
 hipError_t Launch<T>::accuracy(const CsrDev &A, const T *b, const T *x, T *out2,
                                RedWs<T> *ws, hipStream_t s) {
+  const int spmv_grid_ = grid_rows(A.nrb);
   CGX_SPMV_SWITCH(spmv_variant<T>(A), k_accuracy, args(A), (const T *)A.val, b, x, out2, ws);
 }
 template <typename T>

@@ -73,6 +73,7 @@ struct cgx_ctx {
   ncclComm *comm = nullptr;
   cgx::HostComm *host = nullptr;
   int rank = 0, world = 1;
+  hipStream_t cstream = nullptr;  // RCCL halo exchange, overlapped with interior rows
 };
 
 struct cgx_csr {
@@ -90,6 +91,11 @@ struct cgx_csr {
   void *d_sell_sl = nullptr, *d_sell_dict = nullptr, *d_sell_idx = nullptr;
   void *d_sell_val = nullptr;
   void *d_sell_order = nullptr;
+  // partitioned SELL matrix: slices without ghost columns, then those with
+  // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
+  int *d_split = nullptr;
+  int split_ni = 0, split_nb = 0;
+  hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
   int64_t sell_padded = 0;
 };
 
@@ -129,6 +135,10 @@ struct cgx_cg {
 namespace cgx {
 // cgx_dist.cpp
 int dist_halo_exchange(cgx_csr *A, void *d_vec_ext, hipStream_t s);
+// Overlapped form: pack on s, exchange on the context's comm stream (RCCL)
+// or synchronously (host transport); dist_halo_wait makes s wait for it.
+int dist_halo_post(cgx_csr *A, void *d_vec_ext, hipStream_t s, bool *async);
+int dist_halo_wait(cgx_csr *A, hipStream_t s);
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s);
 int dist_destroy_halo(cgx_csr *A);
 int dist_comm_destroy(cgx_ctx *ctx);

@@ -196,6 +196,10 @@ int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_begin,
 /* ghost entries this rank receives per iteration */
 int cgx_csr_halo_info(cgx_csr *csr, int64_t *ghosts, int *neighbours);
 /* Reduce a host double over ranks (sum); utility for tests. */
+/* Slices of a partitioned SELL matrix without / with ghost columns: the
+ * SpMV runs the interior ones while the halo exchange is in flight. Both 0
+ * when the matrix is not split (no SELL copy, or no ghosts). */
+int cgx_csr_split_info(cgx_csr *csr, int *interior_slices, int *boundary_slices);
 int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value);
 
 /* ---- host-only helpers (no device needed; the CPU test-suite drives them) --

@@ -74,6 +74,8 @@ def main():
                                 C.byref(A)))
     ghosts, nbrs = C.c_int64(), C.c_int()
     check(L.cgx_csr_halo_info(A, C.byref(ghosts), C.byref(nbrs)))
+    ni, nb = C.c_int(), C.c_int()
+    check(L.cgx_csr_split_info(A, C.byref(ni), C.byref(nb)))
     b = cga.DeviceArray(q, nl, np.float64)
     x = cga.DeviceArray(q, nl, np.float64)
     check(L.cgx_iota(q.handle, F64, b.ptr, nl, float(begin)))
@@ -86,7 +88,8 @@ def main():
     acc = C.c_double()
     check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
     parts = [None] * world
-    dist.all_gather_object(parts, (x.download().tolist(), int(ghosts.value), int(nbrs.value)))
+    dist.all_gather_object(parts, (x.download().tolist(), int(ghosts.value), int(nbrs.value),
+                                   (ni.value, nb.value)))
     if rank == 0:
         from oracle import oracle as O
         xg = np.concatenate([np.array(p[0]) for p in parts])
@@ -97,7 +100,8 @@ def main():
         print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode, "grid": g, "bodies": bodies.value,
                           "oracle_bodies": res.iterations, "rel_err": relerr,
                           "accuracy": acc.value, "ghosts": [p[1] for p in parts],
-                          "neighbours": [p[2] for p in parts], "ok": ok}), flush=True)
+                          "neighbours": [p[2] for p in parts],
+                          "split": [p[3] for p in parts], "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)
     L.cgx_csr_destroy(A)
     q.close()

@@ -49,3 +49,5 @@ def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
         # slab partition of a 3-D grid: every rank has ghosts, inner ranks 2 nbrs
         assert all(g > 0 for g in r["ghosts"])
         assert r["neighbours"][0] == 1
+        # the SELL copy is split: interior slices run while the halo travels
+        assert all(ni > 0 and nb > 0 for ni, nb in r["split"]), r["split"]
