@@ -65,7 +65,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--grid", type=int, default=256, help="n of the n^3 grid per GPU")
+    ap.add_argument("--grid", type=int, default=256,
+                    help="n of the n^3 grid per GPU (weak), or of the global grid (--strong)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one global n^3 grid split into z-slabs over the GPUs "
+                         "(e.g. --grid 512, SURVEY §8(e)); default is weak scaling")
     ap.add_argument("--poll", type=int, default=64, help="iterations per host poll")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -118,8 +122,14 @@ def main():
     L = lib()
     q = cga.Queue(dev)
     n3 = args.grid
-    nz_global = n3 * world
-    n_local = n3 * n3 * n3
+    if args.strong:
+        if n3 % world:
+            raise SystemExit(f"--strong needs the grid ({n3}) divisible by the GPU count ({world})")
+        nz_global = n3
+        n_local = n3 * n3 * (n3 // world)
+    else:
+        nz_global = n3 * world
+        n_local = n3 * n3 * n3
     row_begin = rank * n_local
     n_global = n_local * world
 
@@ -215,7 +225,8 @@ def main():
             try:
                 meta = json.load(open(pmc))
                 # PMC bytes of this very kernel: same per-GPU grid, variant, mode
-                if (meta.get("grid") == n3 and meta.get("spmv_variant") == variant.value
+                if (meta.get("grid") == n3 and not args.strong
+                        and meta.get("spmv_variant") == variant.value
                         and meta.get("kernel") == roof["kernel"]):
                     roof["traffic"] = meta.get("hbm_bytes_per_launch")
                     roof["traffic_source"] = "profiles/pmc_spmv_dot.json"
@@ -224,7 +235,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and n3 <= 256:
             cpu = cpu_baseline(n3, min(args.cpu_threads, os.cpu_count() or 1), args.cpu_budget_s)
         line = {
             "metric": "CG iterations/sec + achieved HBM GB/s, 256³ 7-pt Poisson fp64, "
@@ -237,13 +248,15 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "iterations_per_s": round(its, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (3-D 7-point Dirichlet Poisson CSR generated in HBM, "
                     "b_i = i + 1, x0 = 0)",
-            "config": {"workload": f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x"
-                                   f"{nz_global}), CSR fp64/int32 input, SpMV in the "
+            "config": {"workload": (f"3D 7-pt Poisson {n3}^3 global, {nz_global // world} z-planes "
+                                    f"per GPU" if args.strong else
+                                    f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x"
+                                    f"{nz_global})") + ", CSR fp64/int32 input, SpMV in the "
                                    "per-matrix best format",
                        "rows_global": n_global, "nnz_global": nnz_global,
                        "bytes_per_iteration": b_alg(n_global, nnz_global),

@@ -165,15 +165,15 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
     bool async = false;
     if ((rc = dist_halo_post(A, p, s, &async))) return rc;
     const int gi = Launch<T>::slice_grid(A->split_ni);
+    // one timed region: interior slices, the wait for the halo, boundary slices
     if ((rc = timed(cg, 1, s, [&] {
-           return Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
-                                             ws, s, rev);
-         })))
-      return rc;
-    if (async && (rc = dist_halo_wait(A, s))) return rc;
-    if ((rc = timed(cg, 1, s, [&] {
-           return Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb, gi, p,
-                                             Ap, st, slot, ws, s, rev);
+           hipError_t e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap,
+                                                     st, slot, ws, s, rev);
+           if (e == hipSuccess && async) e = hipStreamWaitEvent(s, A->ev_halo, 0);
+           if (e == hipSuccess)
+             e = Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb, gi, p,
+                                            Ap, st, slot, ws, s, rev);
+           return e;
          })))
       return rc;
     *np = gi + Launch<T>::slice_grid(A->split_nb);

@@ -206,11 +206,6 @@ int dist_halo_post(cgx_csr *A, void *vec_ext, hipStream_t s, bool *async) {
   return CGX_OK;
 }
 
-int dist_halo_wait(cgx_csr *A, hipStream_t s) {
-  CGX_HIP(hipStreamWaitEvent(s, A->ev_halo, 0));
-  return CGX_OK;
-}
-
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s) {
   if (!multi(ctx)) return CGX_OK;
   if (ctx->host) {

@@ -135,10 +135,10 @@ struct cgx_cg {
 namespace cgx {
 // cgx_dist.cpp
 int dist_halo_exchange(cgx_csr *A, void *d_vec_ext, hipStream_t s);
-// Overlapped form: pack on s, exchange on the context's comm stream (RCCL)
-// or synchronously (host transport); dist_halo_wait makes s wait for it.
+// Overlapped form: pack on s, exchange on the context's comm stream (RCCL,
+// *async = true: s must wait on A->ev_halo before reading the ghosts) or
+// synchronously (host transport).
 int dist_halo_post(cgx_csr *A, void *d_vec_ext, hipStream_t s, bool *async);
-int dist_halo_wait(cgx_csr *A, hipStream_t s);
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s);
 int dist_destroy_halo(cgx_csr *A);
 int dist_comm_destroy(cgx_ctx *ctx);
