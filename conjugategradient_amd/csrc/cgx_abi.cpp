@@ -233,6 +233,8 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   T *P[4] = {(T *)cg->p, (T *)cg->pk[0], (T *)cg->pk[1], (T *)cg->pk[2]};
   T *p = P[slot], *pn = P[(slot + 1) & 3];
   T *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
+  // r is updated in place (a ping-pong between two buffers measured 5-9%
+  // slower in update_r)
   int rc;
   const int npr = Launch<T>::update_parts(cg->n);
   // sweep directions: each kernel starts where the previous one ended

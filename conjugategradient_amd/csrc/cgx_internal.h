@@ -122,7 +122,7 @@ template <typename T> struct Launch {
   // np_pap > 0: p.Ap from the spmv_dot partials; 0: from st->pAp[slot]
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0,
-                             int rev = 0);
+                             int rev = 0, const T *rin = nullptr);  // rin: r_old (null: r)
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
   // SpMV + p.Ap over `count` SELL slices listed at `list` (device), partials

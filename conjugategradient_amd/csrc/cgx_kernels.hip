@@ -1360,7 +1360,8 @@ template <> struct Vec2<float> { using V = float2; };
 // FUSED: kernel 2 of 2 of the fused iteration, which also runs the stop rule
 // (CG.hpp:396-404, 410-417, 436) and marks body k's x update as pending.
 template <typename T, bool FUSED>
-__global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ r,
+// rin == r: in place (modes 1, 2); else r ping-pongs between two buffers.
+__global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T *r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
                                                      RedWs<T> *ws, int np_pap, int rev) {
@@ -1383,6 +1384,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
   const int64_t n2 = n >> 1;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   V *r2 = reinterpret_cast<V *>(r);
+  const V *ri2 = reinterpret_cast<const V *>(rin);
   const V *a2 = reinterpret_cast<const V *>(Ap);
   T acc = T(0);
   auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
@@ -1391,7 +1393,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
     V rv[4], av[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      rv[u] = r2[E(i + u * stride)];
+      rv[u] = ri2[E(i + u * stride)];
       av[u] = a2[E(i + u * stride)];
     }
 #pragma unroll
@@ -1404,7 +1406,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
     }
   }
   for (; i < n2; i += stride) {
-    V rv = r2[E(i)];
+    V rv = ri2[E(i)];
     const V av = a2[E(i)];
     rv.x = rv.x - alpha * av.x;
     rv.y = rv.y - alpha * av.y;
@@ -1413,7 +1415,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, T *__restrict__ 
     acc += rv.y * rv.y;
   }
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const T v = r[n - 1] - alpha * Ap[n - 1];
+    const T v = rin[n - 1] - alpha * Ap[n - 1];
     r[n - 1] = v;
     acc += v * v;
   }
@@ -1965,13 +1967,15 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
 }
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
-                               RedWs<T> *ws, hipStream_t s, bool fused, int np_pap, int rev) {
+                               RedWs<T> *ws, hipStream_t s, bool fused, int np_pap, int rev,
+                               const T *rin) {
+  if (!rin) rin = r;
   if (fused) {
-    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws, 0, 0);
+    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, rin, r,
+                       Ap, st, slot, ws, 0, 0);
   } else {
-    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, r, Ap,
-                       st, slot, ws, np_pap, rev);
+    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, rin,
+                       r, Ap, st, slot, ws, np_pap, rev);
   }
   return hipGetLastError();
 }
