@@ -103,6 +103,9 @@ _SIGS = {
                            C.POINTER(C.POINTER(_i32)), C.POINTER(C.POINTER(_i32)),
                            C.POINTER(C.POINTER(C.c_double))]),
     "cgx_mm_write_lower": (_i32, [C.c_char_p, _i64, _vp, _vp, _vp, _i32]),
+    "cgx_sellp_plan": (_i32, [_vp, _vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
+                              C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
+                              C.POINTER(_i32)]),
     "cgx_sell_plan": (_i32, [_vp, _vp, _i64, _i32, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
                              C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
                              C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(_i64)]),

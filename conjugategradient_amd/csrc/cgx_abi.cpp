@@ -695,7 +695,7 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 
 void free_sell(cgx_csr *A) {
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
-                   &A->d_sell_order, (void **)&A->d_split}) {
+                   &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -705,6 +705,8 @@ void free_sell(cgx_csr *A) {
   A->dev.sval = nullptr;
   A->dev.nsl = 0;
   A->dev.sorder = nullptr;
+  A->dev.sell_kind = 0;
+  A->dev.smask = nullptr;
   A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
@@ -784,6 +786,94 @@ static bool sell_plan_host(int64_t n, const int *rowptr, const int *col, int R,
   return true;
 }
 
+// SELL-P plan (2 rows per lane, slices of 128 rows): per slice the sorted
+// union of its (col - row) offsets, at most kSellPatMax; rows must have
+// strictly ascending columns (then a row's set slots are its CSR order).
+// Padding bound as in sell_plan_host. maxw: the widest pattern.
+static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
+                            std::vector<SellSlice> &sl, std::vector<int> &pool,
+                            int64_t &voff_total, int &maxw) {
+  const int64_t nnz = (int64_t)rowptr[n] - rowptr[0];
+  const int64_t H = 2 * kSellRows;
+  if (nnz < 1 || n + H >= (int64_t(1) << 31)) return false;
+  const int64_t nsl = (n + H - 1) / H;
+  sl.assign((size_t)nsl, SellSlice{});
+  pool.clear();
+  std::vector<std::pair<std::vector<int>, int>> seen;
+  std::vector<int> P;
+  int64_t voff = 0, padded = 0;
+  maxw = 0;
+  for (int64_t q = 0; q < nsl; ++q) {
+    const int64_t r0 = q * H, r1 = std::min(n, r0 + H);
+    P.clear();
+    for (int64_t i = r0; i < r1; ++i) {
+      for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        if (k > rowptr[i] && col[k] <= col[k - 1]) return false;  // unsorted or duplicate
+        const int off = col[k] - (int)i;
+        auto it = std::lower_bound(P.begin(), P.end(), off);
+        if (it == P.end() || *it != off) {
+          if ((int)P.size() == kSellPatMax) return false;
+          P.insert(it, off);
+        }
+      }
+    }
+    const int W = std::max<int>(1, (int)P.size());
+    if (P.empty()) P.push_back(0);
+    int base = -1;
+    for (auto &e : seen)
+      if (e.first == P) {
+        base = e.second;
+        break;
+      }
+    if (base < 0) {
+      base = (int)pool.size();
+      pool.insert(pool.end(), P.begin(), P.end());
+      if (seen.size() >= 16) seen.erase(seen.begin());
+      seen.emplace_back(P, base);
+    }
+    sl[(size_t)q] = SellSlice{voff, 0, base, W};
+    voff += H * W;
+    padded += (r1 - r0) * W;
+    maxw = std::max(maxw, W);
+  }
+  if (padded > nnz + nnz / 4 + 4096) return false;
+  pool.resize(pool.size() + kSellPatMax, 0);  // the kernel reads up to 7 slots past a pattern
+  voff_total = voff;
+  return true;
+}
+
+extern "C" int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+                              int64_t **slices, int64_t *npat, int **pat, int64_t *value_slots,
+                              int *max_width) {
+  CGX_REQUIRE(h_rowptr && h_col && nsl && slices && npat && pat && value_slots && max_width,
+              CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(n >= 1, CGX_EINVAL, "n=%lld", (long long)n);
+  std::vector<SellSlice> sl;
+  std::vector<int> pool;
+  int64_t voff = 0;
+  int mw = 0;
+  *nsl = *npat = *value_slots = 0;
+  *max_width = 0;
+  *slices = nullptr;
+  *pat = nullptr;
+  if (n < 2 || !sellp_plan_host(n, h_rowptr, h_col, sl, pool, voff, mw)) return CGX_OK;
+  *slices = (int64_t *)std::malloc(sl.size() * 4 * sizeof(int64_t));
+  *pat = (int *)std::malloc(pool.size() * sizeof(int));
+  CGX_REQUIRE(*slices && *pat, CGX_ENOMEM, "host allocation failed");
+  for (size_t q = 0; q < sl.size(); ++q) {
+    (*slices)[4 * q] = sl[q].voff;
+    (*slices)[4 * q + 1] = sl[q].ioff;
+    (*slices)[4 * q + 2] = sl[q].dict;
+    (*slices)[4 * q + 3] = sl[q].width;
+  }
+  std::memcpy(*pat, pool.data(), pool.size() * sizeof(int));
+  *nsl = (int64_t)sl.size();
+  *npat = (int64_t)pool.size();
+  *value_slots = voff;
+  *max_width = mw;
+  return CGX_OK;
+}
+
 extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int rows_per_lane,
                              int64_t *nsl,
                              int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,
@@ -852,12 +942,17 @@ static std::vector<int> sell_visit_order(int64_t nsl, int64_t H, int64_t P) {
 // CSR-stream schedule and this returns CGX_OK. Errors are device failures
 // only. $CGX_SELL=0 disables it, =1 / =2 selects R.
 int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
+  // R: 1 / 2 dictionary SELL with R rows per lane, 3 SELL-P (2 rows per
+  // lane), 0 the default: SELL-P where the matrix qualifies, else R = 2
+  bool fallback = false;
   if (R == 0) {
-    R = kSellDefaultR;
+    R = 3;
+    fallback = true;
     if (const char *env = std::getenv("CGX_SELL")) {
       R = std::atoi(env);
       if (R == 0) return CGX_OK;
-      if (R != 1 && R != 2) R = kSellDefaultR;
+      if (R < 1 || R > 3) R = 3;
+      fallback = R == 3;
     }
   }
   free_sell(A);
@@ -884,9 +979,20 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   std::vector<int> pool;
   std::vector<unsigned long long> idx;
   int64_t voff = 0;
-  if (!sell_plan_host(n, h_rowptr, h_col, R, sl, pool, idx, voff)) return CGX_OK;
+  int kind = 0, maxw = 0;
+  const int64_t nx = A->dev.n + A->halo.n_ghost;
+  if (R == 3) {
+    if (nx >= 2 && sellp_plan_host(n, h_rowptr, h_col, sl, pool, voff, maxw)) {
+      kind = maxw <= 8 ? 1 : 2;
+      R = 2;
+    } else if (fallback) {
+      R = 2;
+    } else {
+      return CGX_OK;
+    }
+  }
+  if (!kind && !sell_plan_host(n, h_rowptr, h_col, R, sl, pool, idx, voff)) return CGX_OK;
   const int64_t nsl = (int64_t)sl.size();
-  pool.resize(pool.size() + kSellMaxDict, 0);  // every lane of the last dictionary reads in bounds
   const size_t es = dtype_size(A->dtype);
   hipError_t e = hipMalloc(&A->d_sell_sl, sl.size() * sizeof(SellSlice));
   if (e == hipSuccess) e = hipMalloc(&A->d_sell_dict, pool.size() * sizeof(int));
@@ -901,6 +1007,8 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
                        hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !idx.empty())
     e = hipMemcpyAsync(A->d_sell_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && kind)  // one mask per row, rows padded to whole slices
+    e = hipMalloc(&A->d_sell_mask, (size_t)(nsl * 2 * kSellRows) * (kind == 2 ? 4 : 1));
   if (e != hipSuccess) {
     free_sell(A);
     return hip_fail(e, "cgx_csr_create(SELL copy)");
@@ -932,10 +1040,19 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   A->dev.sval = A->d_sell_val;
   A->dev.nsl = nsl;
   A->dev.sell_r = R;
+  A->dev.sell_kind = kind;
+  A->dev.smask = A->d_sell_mask;
+  A->dev.nx = nx;
   A->dev.sell_maxw = 0;
   for (const SellSlice &m : sl) A->dev.sell_maxw = std::max(A->dev.sell_maxw, m.width);
   A->sell_padded = voff;
-  if (A->dtype == CGX_F32)
+  if (kind && A->dtype == CGX_F32)
+    e = Launch<float>::sellp_pack(A->dev, (const float *)A->dev.val, (float *)A->d_sell_val,
+                                  A->d_sell_mask, s);
+  else if (kind)
+    e = Launch<double>::sellp_pack(A->dev, (const double *)A->dev.val, (double *)A->d_sell_val,
+                                   A->d_sell_mask, s);
+  else if (A->dtype == CGX_F32)
     e = Launch<float>::sell_pack(A->dev, (const float *)A->dev.val, (float *)A->d_sell_val, s);
   else
     e = Launch<double>::sell_pack(A->dev, (const double *)A->dev.val, (double *)A->d_sell_val, s);
@@ -949,23 +1066,24 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
 
 extern "C" int cgx_csr_set_sell(cgx_csr *A, int rows_per_lane) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
-  CGX_REQUIRE(rows_per_lane >= 0 && rows_per_lane <= 2, CGX_EINVAL,
-              "rows_per_lane must be 0 (drop the SELL copy), 1 or 2");
+  CGX_REQUIRE(rows_per_lane >= 0 && rows_per_lane <= 3, CGX_EINVAL,
+              "layout must be 0 (drop the SELL copy), 1 or 2 (dictionary SELL, rows per "
+              "lane) or 3 (SELL-P)");
   DeviceGuard g(A->ctx->device);
   if (rows_per_lane == 0) {
     free_sell(A);
-    if (A->dev.variant & 2048) A->dev.variant = 0;
+    if (A->dev.variant & (2048 | 8192)) A->dev.variant = 0;
     return CGX_OK;
   }
   int rc = build_sell(A, nullptr, nullptr, rows_per_lane);
   if (rc) return rc;
-  if (!A->dev.sl && (A->dev.variant & 2048)) A->dev.variant = 0;
+  if (!A->dev.sl && (A->dev.variant & (2048 | 8192))) A->dev.variant = 0;
   return CGX_OK;
 }
 
 extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
-  if (has_sell) *has_sell = A->dev.sl ? A->dev.sell_r : 0;
+  if (has_sell) *has_sell = !A->dev.sl ? 0 : (A->dev.sell_kind ? 3 : A->dev.sell_r);
   if (padded) *padded = A->sell_padded;
   return CGX_OK;
 }
@@ -973,7 +1091,7 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
 static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
                            68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
-                           267, 2048, 2050, 2056, 2058, 6144, 6146};
+                           267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578};
   for (int k : ok)
     if (k == v) return true;
   return false;
@@ -982,7 +1100,7 @@ static bool known_variant(int v) {
 extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
   CGX_REQUIRE(known_variant(variant), CGX_EINVAL, "unknown SpMV variant %d", variant);
-  CGX_REQUIRE(!(variant & 2048) || A->dev.sl, CGX_EUNSUPPORTED,
+  CGX_REQUIRE(!(variant & (2048 | 8192)) || A->dev.sl, CGX_EUNSUPPORTED,
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
   A->dev.variant = variant;
   return CGX_OK;
@@ -997,7 +1115,7 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
 int autotune_spmv(cgx_csr *A) {
   if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
     A->dev.variant = std::atoi(env);
-    if (!(A->dev.variant & 2048)) free_sell(A);
+    if (!(A->dev.variant & (2048 | 8192))) free_sell(A);
     return CGX_OK;
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
@@ -1067,7 +1185,7 @@ int autotune_spmv(cgx_csr *A) {
     if (p) (void)hipFree(p);
   CGX_HIP(e);
   A->dev.variant = best_v;
-  if (!(best_v & 2048)) free_sell(A);
+  if (!(best_v & (2048 | 8192))) free_sell(A);
   return CGX_OK;
 }
 

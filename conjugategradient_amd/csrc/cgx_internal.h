@@ -76,6 +76,7 @@ constexpr int kSellRows = 64;
 constexpr int kSellMaxDict = 64;    // distinct (col - row) per slice: one VGPR
 constexpr int kSellMaxWidth = 64;   // longest row of a slice
 constexpr unsigned kSellPad = 0xff;
+constexpr int kSellPatMax = 32;   // SELL-P: offsets per slice pattern (u32 masks)
 constexpr int kSellDefaultR = 2;    // rows per lane of the SELL copy cgx_csr_create builds
                                     // (2: 16-byte loads, profiles/r01_tune_sell2.log)
 struct SellSlice {
@@ -105,6 +106,11 @@ struct CsrDev {
   int sell_maxw = 0;  // widest slice
   int sell_r = 1;     // rows per lane of the SELL copy
   const int *sorder = nullptr;  // visit order of the slices (null: index order)
+  // SELL-P (pattern) copy: per-slice offset pattern (in sdict) and one slot
+  // mask per row (u8 or u32); 0: dictionary SELL, 1: u8 masks, 2: u32 masks
+  int sell_kind = 0;
+  const void *smask = nullptr;
+  int64_t nx = 0;  // length of the gathered vector (n, + ghosts when partitioned)
 };
 
 template <typename T> struct Launch {
@@ -161,6 +167,8 @@ template <typename T> struct Launch {
   static hipError_t gather(const T *src, const int *idx, int64_t n, T *dst,
                            hipStream_t s);
   static hipError_t sell_pack(const CsrDev &A, const T *val, T *sval, hipStream_t s);
+  static hipError_t sellp_pack(const CsrDev &A, const T *val, T *sval, void *mask,
+                               hipStream_t s);
 };
 
 // axpby modes

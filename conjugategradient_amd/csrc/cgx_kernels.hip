@@ -213,6 +213,8 @@ struct CsrArgs {
   const int *__restrict__ sorder;
   int rev;       // per launch: walk the rows high to low (alternating sweeps)
   int part_off;  // per launch: first partial slot of k_spmv_dot (split launches)
+  const void *smask;  // SELL-P slot masks
+  int64_t nx;         // gathered vector length
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -265,15 +267,32 @@ template <bool NT, typename P> __device__ __forceinline__ P ldg(const P *p) {
 // Where the SpMV takes its x_j from: a stored vector, or p_j computed on the
 // fly as r_j + beta * p_old_j (the fused iteration; the same expression the
 // reference evaluates for p, CG.hpp:418, so the value is bit-identical).
+// pair(c): elements c and c + 1 in one load of 2 T at T's alignment (SELL-P)
+template <typename T> struct PairU;
+template <> struct PairU<double> {
+  typedef double V __attribute__((ext_vector_type(2), aligned(8)));
+};
+template <> struct PairU<float> { typedef float V __attribute__((ext_vector_type(2), aligned(4))); };
 template <typename T> struct GatherX {
   const T *__restrict__ x;
   __device__ __forceinline__ T operator()(int c) const { return x[c]; }
+  __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
+    return *reinterpret_cast<const typename PairU<T>::V *>(x + c);
+  }
 };
 template <typename T> struct GatherP {
   const T *__restrict__ r;
   const T *__restrict__ pp;
   T beta;
   __device__ __forceinline__ T operator()(int c) const { return r[c] + beta * pp[c]; }
+  __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
+    using U = typename PairU<T>::V;
+    const U a = *reinterpret_cast<const U *>(r + c), b = *reinterpret_cast<const U *>(pp + c);
+    U o;
+    o.x = a.x + beta * b.x;
+    o.y = a.y + beta * b.y;
+    return o;
+  }
 };
 
 template <int V>
@@ -1081,17 +1100,89 @@ __device__ __forceinline__ void spmv_sell2(const CsrArgs &A, const Gather &x, Ep
     sell_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
 
+// SELL-P (variant bit 8192; 16384: u32 masks): the dictionary SELL layout
+// with 2 rows per lane, but each slice stores its sorted offset pattern
+// o_0 < ... < o_{W-1} once (read as scalars) and every row a mask of the
+// slots it uses; values sit in pattern slots (zero where a row has no
+// entry). Slot j of both rows of a lane gathers x[r0 + o_j] and
+// x[r0 + 1 + o_j] as one unaligned pair load (clamped to the vector; a
+// clamped end selects the other half). Rows sum their set slots in
+// ascending offset order = their CSR order (columns strictly ascending,
+// checked at build), so the sums are bit-identical. Index stream: one mask
+// per row (1 or 4 bytes) instead of 8 bytes.
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void sellp_slice2(const CsrArgs &A, const Gather &x, Epi &epi, int s) {
+  constexpr bool NT = (V & 2) != 0;
+  using PV = typename PairOf<T>::V;
+  using MT = typename std::conditional<(V & 16384) != 0, unsigned, unsigned char>::type;
+  const PV *__restrict__ sval = static_cast<const PV *>(A.sval);
+  const MT *__restrict__ smask = static_cast<const MT *>(A.smask);
+  const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
+  const auto *pat = (const __attribute__((address_space(4))) int *)A.sdict;
+  const int lane = threadIdx.x & 63;
+  const int si = __builtin_amdgcn_readfirstlane(s);
+  const int64_t voff = cs[si].voff;
+  const int pbase = cs[si].dict, W = cs[si].width;
+  const int r0 = si * (2 * kSellRows) + 2 * lane;
+  const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
+  const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
+  epi.pre2(rc0, rc1);
+  const unsigned m0 = smask[r0], m1 = smask[r0 + 1];  // rows past n: mask 0 (array padded)
+  const int nxm2 = (int)A.nx - 2;
+  T acc0 = T(0), acc1 = T(0);
+  for (int c = 0; c < W; c += 8) {
+    const PV *vp = sval + (voff >> 1) + (int64_t)c * kSellRows + lane;
+    PV v[8];
+    T g0[8], g1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ldg<NT>(vp + min(j, W - 1 - c) * kSellRows);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = pat[pbase + min(c + j, W - 1)];
+      const int base = r0 + o;
+      const int cb = min(max(base, 0), nxm2);
+      if constexpr ((V & 16) != 0) {
+        g0[j] = T(cb & 1);
+        g1[j] = T(cb & 2);
+      } else {
+        const auto g = x.pair(cb);
+        g0[j] = base <= nxm2 ? g.x : g.y;
+        g1[j] = base >= 0 ? g.y : g.x;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int b = c + j;
+      const bool in = b < W;
+      const T t0 = acc0 + v[j].x * g0[j];
+      const T t1 = acc1 + v[j].y * g1[j];
+      acc0 = (in && ((m0 >> (b & 31)) & 1u)) ? t0 : acc0;
+      acc1 = (in && ((m1 >> (b & 31)) & 1u)) ? t1 : acc1;
+    }
+  }
+  epi.row2(r0, acc0, acc1, l0, l1);
+}
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sellp(const CsrArgs &A, const Gather &x, Epi &epi) {
+  int s, step, end, lo;
+  sell_range((int)A.nsl, s, step, end, lo);
+  for (; s < end; s += step)
+    sellp_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
 using LdsOf = typename std::conditional<
-    (V & 2048) != 0, SellLds<T>,
+    (V & (2048 | 8192)) != 0, SellLds<T>,
     typename std::conditional<(V & 512) != 0, WaveLds<T>, SpmvLds<T, TileOf<V>::tile>>::type>::type;
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
                                          const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
-  if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
+  if constexpr ((V & 8192) != 0) spmv_sellp<T, V, Epi, Gather>(A, x, epi);
+  else if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0) spmv_sell<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
@@ -1589,6 +1680,42 @@ __global__ __launch_bounds__(kBlock) void k_sell_pack(int64_t n, int64_t nsl, in
   }
 }
 
+// SELL-P values and masks: row i of slice q puts entry (col c) in the slot of
+// offset c - i in the slice's pattern (both ascending), zero elsewhere, and
+// sets that slot's mask bit. Rows past n: zeros, mask 0.
+template <typename T, typename MT>
+__global__ __launch_bounds__(kBlock) void k_sellp_pack(int64_t n, int64_t nsl,
+                                                       const int *__restrict__ rowptr,
+                                                       const int *__restrict__ col,
+                                                       const T *__restrict__ val,
+                                                       const SellSlice *__restrict__ sl,
+                                                       const int *__restrict__ pat,
+                                                       T *__restrict__ sval, MT *__restrict__ mask) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t H = 2 * kSellRows;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nsl * H; i += stride) {
+    const SellSlice m = sl[i / H];
+    const int li = (int)(i % H), l = li >> 1, r = li & 1;
+    const int *P = pat + m.dict;
+    int a = 0, e = 0;
+    if (i < n) {
+      a = rowptr[i];
+      e = rowptr[i + 1];
+    }
+    unsigned bits = 0;
+    int k = a;
+    for (int j = 0; j < m.width; ++j) {
+      T v = T(0);
+      if (k < e && col[k] - (int)i == P[j]) {
+        v = val[k++];
+        bits |= 1u << j;
+      }
+      sval[m.voff + ((int64_t)j * kSellRows + l) * 2 + r] = v;
+    }
+    mask[i] = (MT)bits;
+  }
+}
+
 // Poisson rows [row_begin, row_end): columns ascending (-z,-y,-x,d,+x,+y,+z).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_poisson(int dim, int nx, int ny, int nz,
@@ -1629,7 +1756,8 @@ inline int elem_grid(int64_t n, int per_thread) {
 
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
-                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0};
+                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
+                 A.smask,  A.nx > 0 ? A.nx : A.n};
 }
 
 }  // namespace
@@ -1827,9 +1955,10 @@ constexpr int64_t kNtMinBytes = int64_t(256) << 20;
 
 template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   if (v < 0 && A.variant > 0) v = A.variant;  // chosen by cgx_csr_create's autotune
-  if (v >= 0 && (v & 2048)) {
+  if (v >= 0 && (v & (2048 | 8192))) {
     // the variant follows the SELL copy's layout: bit 4096 for 2 rows per
     // lane; pipelined (bit 8) for 1 row per lane and slices <= 8 wide
+    if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
     v = -1;  // no SELL copy: CSR-stream
@@ -1902,6 +2031,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 2058: CGX_LAUNCH_V(KERNEL, 2058, __VA_ARGS__);                               \
     case 6144: CGX_LAUNCH_V(KERNEL, 6144, __VA_ARGS__);                               \
     case 6146: CGX_LAUNCH_V(KERNEL, 6146, __VA_ARGS__);                               \
+    case 8192: CGX_LAUNCH_V(KERNEL, 8192, __VA_ARGS__);                               \
+    case 8194: CGX_LAUNCH_V(KERNEL, 8194, __VA_ARGS__);                               \
+    case 24576: CGX_LAUNCH_V(KERNEL, 24576, __VA_ARGS__);                             \
+    case 24578: CGX_LAUNCH_V(KERNEL, 24578, __VA_ARGS__);                             \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -1933,7 +2066,7 @@ hipError_t Launch<T>::spmv_dot_slices(const CsrDev &A, const int *list, int coun
                                       const T *p, T *Ap, CgScalars<T> *st, int slot,
                                       RedWs<T> *ws, hipStream_t s, int rev) {
   const int v = spmv_variant<T>(A);
-  if (!(v & 2048) || count < 1) return hipErrorInvalidValue;
+  if (!(v & (2048 | 8192)) || count < 1) return hipErrorInvalidValue;
   CsrArgs a = args(A);
   a.sorder = list;
   a.nsl = count;
@@ -1961,6 +2094,7 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 2074: CGX_LAUNCH_V(k_spmv_dot, 2074, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 6160: CGX_LAUNCH_V(k_spmv_dot, 6160, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 6162: CGX_LAUNCH_V(k_spmv_dot, 6162, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 8210: CGX_LAUNCH_V(k_spmv_dot, 8210, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -2073,6 +2207,19 @@ hipError_t Launch<T>::sell_pack(const CsrDev &A, const T *val, T *sval, hipStrea
 
 int launch_variant(const CsrDev &A, int dtype) {
   return dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A);
+}
+
+template <typename T>
+hipError_t Launch<T>::sellp_pack(const CsrDev &A, const T *val, T *sval, void *mask,
+                                 hipStream_t s) {
+  const int g = elem_grid(A.nsl * kSellRows * 2, 4);
+  if (A.sell_kind == 2)
+    hipLaunchKernelGGL((k_sellp_pack<T, unsigned>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
+                       A.rowptr, A.col, val, A.sl, A.sdict, sval, (unsigned *)mask);
+  else
+    hipLaunchKernelGGL((k_sellp_pack<T, unsigned char>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
+                       A.rowptr, A.col, val, A.sl, A.sdict, sval, (unsigned char *)mask);
+  return hipGetLastError();
 }
 
 template struct Launch<double>;

@@ -91,6 +91,7 @@ struct cgx_csr {
   void *d_sell_sl = nullptr, *d_sell_dict = nullptr, *d_sell_idx = nullptr;
   void *d_sell_val = nullptr;
   void *d_sell_order = nullptr;
+  void *d_sell_mask = nullptr;  // SELL-P slot masks
   // partitioned SELL matrix: slices without ghost columns, then those with
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;

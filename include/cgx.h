@@ -86,11 +86,13 @@ int cgx_csr_variant(cgx_csr *csr, int *variant);
  * with CGX_EUNSUPPORTED when the matrix has none (or it was freed because
  * the autotune chose a CSR-stream variant). */
 int cgx_csr_set_variant(cgx_csr *csr, int variant);
-/* Rebuild the SELL copy with 1 or 2 rows per lane (slices of 64 or 128
- * rows), or drop it (0). A matrix that does not qualify ends without one.
- * Blocking. */
+/* Rebuild the SELL copy: 1 or 2 = dictionary SELL with 1 or 2 rows per
+ * lane (slices of 64 or 128 rows), 3 = SELL-P (slices of 128 rows, one
+ * offset pattern per slice, one slot mask per row), 0 = drop it. A matrix
+ * that does not qualify ends without one. Blocking. */
 int cgx_csr_set_sell(cgx_csr *csr, int rows_per_lane);
-/* Rows per lane of the matrix's SELL copy (0: none); its padded entry count. */
+/* The matrix's SELL layout (0 none, 1 / 2 dictionary SELL with that many
+ * rows per lane, 3 SELL-P) and its padded entry count. */
 int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
@@ -239,6 +241,13 @@ int cgx_mm_read(const char *path, int threads, int64_t *n, int64_t *nnz, int **r
 int cgx_mm_write_lower(const char *path, int64_t n, const int *rowptr, const int *col,
                        const double *val, int threads);
 
+/* Host-only: the SELL-P layout (2 rows per lane, slices of 128 rows): per
+ * slice {first value slot, 0, first pattern entry, pattern width}; pat[npat]
+ * the sorted (col - row) patterns. *nsl = 0 when the matrix does not
+ * qualify (a pattern wider than 32, unsorted rows, too much padding). */
+int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
+                   int64_t **slices, int64_t *npat, int **pat, int64_t *value_slots,
+                   int *max_width);
 int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int rows_per_lane,
                   int64_t *nsl,
                   int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,

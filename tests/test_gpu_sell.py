@@ -19,7 +19,7 @@ from tests.util import coo_to_csr, irregular_spd, rel
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [2048, 2050, 2056, 2058, 6144, 6146, 13, 15, 0]
+VARIANTS = [2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 13, 15, 0]
 
 
 def banded(n, half=6, seed=1, empty_every=0):
@@ -68,7 +68,7 @@ def _sell_info(m):
     return has.value, padded.value
 
 
-@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("R", [1, 2, 3])   # 3: SELL-P
 @pytest.mark.parametrize("case", ["poisson2d", "poisson3d_ragged", "poisson3d_wide", "banded",
                                   "empty_rows", "tiny"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
@@ -132,7 +132,7 @@ def test_sell_disabled_by_env(queue, oracle, monkeypatch):
     assert _sell_info(A)[0] == 0
 
 
-@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("R", [1, 2, 3])
 def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle, R):
     # padding entries are dropped, not multiplied: an Inf/NaN in x reaches
     # exactly the rows whose real entries touch it, and -0 sums stay -0
@@ -156,7 +156,7 @@ def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle, R):
     np.testing.assert_array_equal(np.signbit(y), np.signbit(ref))
 
 
-@pytest.mark.parametrize("sell", ["1", "2", "0"])
+@pytest.mark.parametrize("sell", ["1", "2", "3", "0"])
 @pytest.mark.parametrize("dim,n", [(2, 64), (3, 20), (3, 0)])
 def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     monkeypatch.setenv("CGX_SELL", sell)
@@ -170,7 +170,7 @@ def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     cg.solve(1e-8)
     v = C.c_int()
     check(lib().cgx_csr_variant(cg.A.schedule(), C.byref(v)))
-    assert bool(v.value & 2048) == (sell != "0")
+    assert bool(v.value & (2048 | 8192)) == (sell != "0")
     assert _sell_info(cg.A)[0] == int(sell)
     xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-8)
     assert abs(cg.iterations - res.iterations) <= 2

@@ -109,6 +109,7 @@ def cases(oracle):
         "tiny": (np.array([0, 1, 3, 4], np.int32), np.array([0, 0, 1, 2], np.int32),
                  np.array([2.0, -1.0, 3.0, 4.0])),
         "wide": banded(777, half=25),   # rows > 8 entries: several index words
+        "mid": banded(901, half=12),    # 25 offsets: SELL-P with u32 masks
     }
 
 
@@ -146,3 +147,117 @@ def test_sell_rejects_scattered_and_long_rows():
     assert sell_plan(rp, cl) is None and sell_plan(rp, cl, 2) is None
     rp, cl, _ = irregular_spd(5_000, seed=5, hub=3000)   # one row of ~3000 entries
     assert sell_plan(rp, cl) is None
+
+
+# ---- SELL-P (pattern slots + row masks, 2 rows per lane) ------------------
+
+def sellp_plan(rp, cl):
+    L = lib()
+    nsl, npat, slots, mw = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int()
+    sl = C.POINTER(C.c_int64)()
+    pat = C.POINTER(C.c_int32)()
+    rp = np.ascontiguousarray(rp, np.int32)
+    cl = np.ascontiguousarray(cl, np.int32)
+    check(L.cgx_sellp_plan(rp.ctypes.data, cl.ctypes.data, len(rp) - 1, C.byref(nsl), C.byref(sl),
+                           C.byref(npat), C.byref(pat), C.byref(slots), C.byref(mw)))
+    if nsl.value == 0:
+        return None
+    out = (np.ctypeslib.as_array(sl, shape=(nsl.value, 4)).copy(),
+           np.ctypeslib.as_array(pat, shape=(npat.value,)).copy(), slots.value, mw.value)
+    for p in (sl, pat):
+        L.cgx_free_host(C.cast(p, C.c_void_p))
+    return out
+
+
+def sellp_pack(rp, cl, vl, sl, pat, slots):
+    """k_sellp_pack: entry of offset o goes to the slot of o in the slice's
+    pattern; mask bit per set slot; rows past n: zeros, mask 0."""
+    n = len(rp) - 1
+    H = 2 * ROWS
+    sval = np.zeros(slots + 8 * H, vl.dtype)
+    mask = np.zeros(len(sl) * H, np.uint32)
+    for q, (voff, _, base, w) in enumerate(sl):
+        P = pat[base:base + w]
+        for li in range(H):
+            i = q * H + li
+            if i >= n:
+                continue
+            l, r = divmod(li, 2)
+            k, e = rp[i], rp[i + 1]
+            bits = 0
+            for j in range(w):
+                if k < e and cl[k] - i == P[j]:
+                    sval[voff + (j * ROWS + l) * 2 + r] = vl[k]
+                    bits |= 1 << j
+                    k += 1
+            assert k == e, "every entry lands in a slot"
+            mask[i] = bits
+    return sval, mask
+
+
+def sellp_emulate(rp, sl, pat, sval, mask, x):
+    """sellp_slice2: pair loads at clamp(r0 + o, 0, nx - 2), halves selected."""
+    n = len(rp) - 1
+    nx = len(x)
+    y = np.zeros(n)
+    lane = np.arange(ROWS)
+    for q, (voff, _, base, w) in enumerate(sl):
+        r0 = q * 2 * ROWS + 2 * lane
+        m0, m1 = mask[r0], mask[r0 + 1]
+        acc0, acc1 = np.zeros(ROWS), np.zeros(ROWS)
+        for c in range(0, w, 8):
+            for j in range(8):
+                jj = min(j, w - 1 - c)
+                vi = voff // 2 + (c + jj) * ROWS + lane
+                assert vi.max() * 2 + 1 < len(sval)
+                v0, v1 = sval[2 * vi], sval[2 * vi + 1]
+                assert base + min(c + j, w - 1) < len(pat)
+                o = pat[base + min(c + j, w - 1)]
+                b = r0 + o
+                cb = np.clip(b, 0, nx - 2)
+                g = np.stack([x[cb], x[cb + 1]])            # the pair load, in bounds
+                g0 = np.where(b <= nx - 2, g[0], g[1])
+                g1 = np.where(b >= 0, g[1], g[0])
+                s = c + j
+                if s < w:
+                    on0 = (m0 >> s) & 1 == 1
+                    on1 = (m1 >> s) & 1 == 1
+                    with np.errstate(invalid="ignore"):
+                        acc0 = np.where(on0, acc0 + v0 * g0, acc0)
+                        acc1 = np.where(on1, acc1 + v1 * g1, acc1)
+        for r, acc in ((0, acc0), (1, acc1)):
+            rows = r0 + r
+            live = rows < n
+            y[rows[live]] = acc[live]
+    return y
+
+
+@pytest.mark.parametrize("case", ["poisson3d_ragged", "poisson2d", "banded", "empty_rows",
+                                  "tiny", "mid"])
+def test_sellp_layout_in_bounds_and_bitexact(oracle, case):
+    rp, cl, vl = cases(oracle)[case]
+    plan = sellp_plan(rp, cl)
+    assert plan is not None, case
+    sl, pat, slots, mw = plan
+    n = len(rp) - 1
+    assert len(sl) == (n + 2 * ROWS - 1) // (2 * ROWS)
+    assert (sl[:, 3] <= 32).all() and mw == sl[:, 3].max()
+    for (_, _, base, w) in sl:           # patterns sorted, strictly ascending
+        P = pat[base:base + w]
+        assert (np.diff(P) > 0).all()
+    sval, mask = sellp_pack(rp, cl, vl, sl, pat, slots)
+    x = np.random.default_rng(2).standard_normal(n)
+    np.testing.assert_array_equal(sellp_emulate(rp, sl, pat, sval, mask, x),
+                                  oracle.spmv(rp, cl, vl, x))
+
+
+def test_sellp_rejects(oracle):
+    # scattered columns, or a band of 51 offsets: patterns wider than 32
+    rp, cl, _ = irregular_spd(20_000, seed=4)
+    assert sellp_plan(rp, cl) is None
+    rp, cl, _ = cases(oracle)["wide"]
+    assert sellp_plan(rp, cl) is None
+    # a row with unsorted columns
+    rp = np.array([0, 2, 3], np.int32)
+    cl = np.array([1, 0, 1], np.int32)
+    assert sellp_plan(rp, cl) is None
