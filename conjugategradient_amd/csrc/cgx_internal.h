@@ -62,7 +62,7 @@ template <typename T> struct RedWs {
   // per-workgroup partials of the iteration's two dots, summed by the NEXT
   // kernel (every workgroup, fixed order): no tail chain in the producer
   T pap_part[2 * kMaxGrid];  // room for the interior + boundary launches of a split SpMV
-  T rr_part[kMaxGrid];
+  T rr_part[2 * kMaxGrid];
 };
 
 // SELL copy of a matrix (built by cgx_csr_create when the matrix qualifies,

@@ -29,6 +29,7 @@
 //    as in the reference's expressions.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "cgx_internal.h"
@@ -1781,7 +1782,18 @@ __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, 
 template <typename T> int Launch<T>::grid_rows(int nrb) {
   return nrb < kMaxGrid ? (nrb < 1 ? 1 : nrb) : kMaxGrid;
 }
-template <typename T> int Launch<T>::grid_elems(int64_t n) { return elem_grid(n, 8); }
+// Streaming kernels: 8 elements per thread, at most kMaxGrid workgroups.
+// $CGX_UPD_GRID (A/B only) caps the grid at another value (<= 2 kMaxGrid).
+template <typename T> int Launch<T>::grid_elems(int64_t n) {
+  static const int cap = [] {
+    const char *e = std::getenv("CGX_UPD_GRID");
+    const int v = e ? std::atoi(e) : 0;
+    return (v >= 64 && v <= 2 * kMaxGrid) ? v : kMaxGrid;
+  }();
+  int64_t g = (n + (int64_t)kBlock * 8 - 1) / ((int64_t)kBlock * 8);
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
 
 
 // Deferred-x iteration (mode 3), kernel 3 of 3 for body k in slot s:
