@@ -115,7 +115,7 @@ struct CsrDev {
 
 template <typename T> struct Launch {
   static int grid_rows(int nrb);
-  static int grid_elems(int64_t n);
+  static int grid_elems(int64_t n, int cap);
   static hipError_t spmv(const CsrDev &A, const T *x, T *y, hipStream_t s);
   static hipError_t cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                             CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,

@@ -1782,14 +1782,14 @@ __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, 
 template <typename T> int Launch<T>::grid_rows(int nrb) {
   return nrb < kMaxGrid ? (nrb < 1 ? 1 : nrb) : kMaxGrid;
 }
-// Streaming kernels: 8 elements per thread, at most kMaxGrid workgroups.
-// $CGX_UPD_GRID (A/B only) caps the grid at another value (<= 2 kMaxGrid).
-template <typename T> int Launch<T>::grid_elems(int64_t n) {
-  static const int cap = [] {
-    const char *e = std::getenv("CGX_UPD_GRID");
-    const int v = e ? std::atoi(e) : 0;
-    return (v >= 64 && v <= 2 * kMaxGrid) ? v : kMaxGrid;
-  }();
+// Streaming kernels: at most `cap` workgroups, each walking its share in a
+// grid-stride loop. Fewer, longer-lived workgroups stream better than the
+// 8-per-CU persistent grid the SpMV uses: k_update_r 256 (1 per CU), the
+// x/p updates 512 (2 per CU; the flushing body keeps 8 streams in flight);
+// A/B in DESIGN.md §4 (gpurun_out r44/r45).
+constexpr int kGridUpdateR = 256;
+constexpr int kGridUpdateP = 512;
+template <typename T> int Launch<T>::grid_elems(int64_t n, int cap) {
   int64_t g = (n + (int64_t)kBlock * 8 - 1) / ((int64_t)kBlock * 8);
   if (g < 1) g = 1;
   return (int)(g > cap ? cap : g);
@@ -2117,16 +2117,19 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
                                const T *rin) {
   if (!rin) rin = r;
   if (fused) {
-    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, rin, r,
+    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n, kMaxGrid)), dim3(kBlock), 0, s,
+                       n, rin, r,
                        Ap, st, slot, ws, 0, 0);
   } else {
-    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n)), dim3(kBlock), 0, s, n, rin,
-                       r, Ap, st, slot, ws, np_pap, rev);
+    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
+                       s, n, rin, r, Ap, st, slot, ws, np_pap, rev);
   }
   return hipGetLastError();
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) { return grid_rows(A.nrb); }
-template <typename T> int Launch<T>::update_parts(int64_t n) { return grid_elems(n); }
+template <typename T> int Launch<T>::update_parts(int64_t n) {
+  return grid_elems(n, kGridUpdateR);  // k_update_r's grid: one r.r partial per workgroup
+}
 template <typename T>
 hipError_t Launch<T>::finalize(const T *part, int np, T *dst, hipStream_t s) {
   CGX_LAUNCH(k_finalize<T>, 1, part, np, dst);
@@ -2146,17 +2149,19 @@ hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int
 template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
                                 int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev) {
-  CGX_LAUNCH(k_update_xp<T>, grid_elems(n), n, x, p, r, st, slot, ws, np_rr, rev);
+  CGX_LAUNCH(k_update_xp<T>, grid_elems(n, kGridUpdateP), n, x, p, r, st, slot, ws, np_rr, rev);
 }
 template <typename T>
 hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
                                      const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
                                      int np_rr, hipStream_t s, int rev) {
   if (slot == 3) {
-    CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n), n, x, p, pn, (const T *)P[0],
+    CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n, kGridUpdateP), n, x, p, pn,
+               (const T *)P[0],
                (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev);
   }
-  CGX_LAUNCH((k_update_p_defer<T, false>), grid_elems(n), n, x, p, pn, (const T *)P[0],
+  CGX_LAUNCH((k_update_p_defer<T, false>), grid_elems(n, kGridUpdateP), n, x, p, pn,
+             (const T *)P[0],
              (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev);
 }
 template <typename T>
