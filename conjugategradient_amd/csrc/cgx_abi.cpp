@@ -1299,9 +1299,11 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
   const size_t next = (size_t)(cg->n + A->halo.n_ghost);
   const size_t stb = cg->dtype == CGX_F32 ? sizeof(CgScalars<float>) : sizeof(CgScalars<double>);
   const size_t wsb = cg->dtype == CGX_F32 ? sizeof(RedWs<float>) : sizeof(RedWs<double>);
-  hipError_t e = hipMalloc(&cg->r, (size_t)cg->n * es);
+  // r and Ap carry one slack element: k_update_r's first loads are clamped
+  // 16-byte pairs, which for n = 1 would reach one element past the end
+  hipError_t e = hipMalloc(&cg->r, ((size_t)cg->n + 1) * es);
   if (e == hipSuccess) e = hipMalloc(&cg->p, next * es);
-  if (e == hipSuccess) e = hipMalloc(&cg->Ap, next * es);
+  if (e == hipSuccess) e = hipMalloc(&cg->Ap, (next + 1) * es);
   if (e == hipSuccess && !A->dist) e = hipMalloc(&cg->p2, (size_t)cg->n * es);
   if (e == hipSuccess) e = hipMalloc(&cg->st, stb);
   if (e == hipSuccess) e = hipMalloc(&cg->ws, wsb);

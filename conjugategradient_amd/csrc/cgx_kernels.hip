@@ -103,6 +103,41 @@ __device__ __forceinline__ T sum_parts(const T *__restrict__ part, int np, T *ld
   return bc;
 }
 
+// LDS-only workgroup barrier: waits for this wave's LDS operations, not for
+// its outstanding global loads (__syncthreads would drain those too).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// sum_parts in two steps, same order and value, for a kernel that issues
+// its first stream loads in between: parts_load puts this thread's partials
+// in registers (all loads issued, none waited for); parts_sum adds them and
+// reduces over the workgroup through LDS with LDS-only barriers, so loads
+// issued after parts_load stay in flight (vmcnt waits in issue order).
+constexpr int kPartsPerThread = 2 * kMaxGrid / kBlock;  // split SpMV: 2 launches
+template <typename T>
+__device__ __forceinline__ void parts_load(const T *__restrict__ part, int np,
+                                           T (&pl)[kPartsPerThread]) {
+#pragma unroll
+  for (int k = 0; k < kPartsPerThread; ++k)  // unconditional (np >= 1): exact vmcnt waits
+    pl[k] = part[min((int)threadIdx.x + k * kBlock, np - 1)];
+}
+template <typename T>
+__device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T *lds) {
+  __shared__ T bc;
+  T v = T(0);
+#pragma unroll
+  for (int k = 0; k < kPartsPerThread; ++k)
+    if ((int)threadIdx.x + k * kBlock < np) v += pl[k];  // sum_parts order
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) lds[w] = v;
+  lds_barrier();
+  if (threadIdx.x == 0) bc = ((lds[0] + lds[1]) + lds[2]) + lds[3];
+  lds_barrier();
+  return bc;
+}
+
 // Grid-wide deterministic reduction. Every workgroup publishes its block sum
 // write-through and takes the ticket of its group (blockIdx % kRedGroups). The
 // last arrival of a group sums the group's partials in workgroup order and
@@ -1463,30 +1498,48 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
   }
   __shared__ T red[4];
   __shared__ int flag;
-  // p.Ap: the spmv_dot partials (single device) or st (fused mode, or
-  // partitioned runs after the all-reduce)
-  const T pAp = (!FUSED && np_pap > 0) ? sum_parts(ws->pap_part, np_pap, red) : st->pAp[slot];
-  const T alpha = st->rxr[slot] / pAp;
-  if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // the record; the deferred x update
-    st->pAp[slot] = pAp;
-    st->alpha[slot] = alpha;
-    st->skip[slot] = 0;
-  }
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   V *r2 = reinterpret_cast<V *>(r);
   const V *ri2 = reinterpret_cast<const V *>(rin);
   const V *a2 = reinterpret_cast<const V *>(Ap);
-  T acc = T(0);
   auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  for (; i + 3 * stride < n2; i += 4 * stride) {
-    V rv[4], av[4];
+  // p.Ap: the spmv_dot partials (single device) or st (fused mode, or
+  // partitioned runs after the all-reduce). The partials' loads go out
+  // first, then this thread's first block of r and Ap (which do not need
+  // alpha), then the partials are summed while that block is in flight.
+  // scalar loads (lgkmcnt): a vector load issued after the prefetch would
+  // make its wait drain the prefetch too
+  const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
+  const T rxr = cst->rxr[slot];
+  const T pAp_st = cst->pAp[slot];
+  T pl[kPartsPerThread];
+  const bool from_parts = !FUSED && np_pap > 0;
+  if (from_parts) parts_load(ws->pap_part, np_pap, pl);
+  V rv[4], av[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      rv[u] = ri2[E(i + u * stride)];
-      av[u] = a2[E(i + u * stride)];
+  for (int u = 0; u < 4; ++u) {  // clamped (r and Ap have a slack element): no branch
+    const int64_t j = E(min(i + u * stride, n2 > 0 ? n2 - 1 : 0));
+    rv[u] = ri2[j];
+    av[u] = a2[j];
+  }
+  const T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
+  const T alpha = rxr / pAp;
+  if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // the record; the deferred x update
+    st->pAp[slot] = pAp;
+    st->alpha[slot] = alpha;
+    st->skip[slot] = 0;
+  }
+  T acc = T(0);
+  for (bool first = true; i + 3 * stride < n2; i += 4 * stride, first = false) {
+    if (!first) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        rv[u] = ri2[E(i + u * stride)];
+        av[u] = a2[E(i + u * stride)];
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1780,7 +1833,12 @@ __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, 
 }
 
 template <typename T> int Launch<T>::grid_rows(int nrb) {
-  return nrb < kMaxGrid ? (nrb < 1 ? 1 : nrb) : kMaxGrid;
+  static const int cap = [] {  // $CGX_SPMV_GRID: A/B only
+    const char *e = std::getenv("CGX_SPMV_GRID");
+    const int v = e ? std::atoi(e) : 0;
+    return (v >= 64 && v <= kMaxGrid) ? v : kMaxGrid;
+  }();
+  return nrb < cap ? (nrb < 1 ? 1 : nrb) : cap;
 }
 // Streaming kernels: at most `cap` workgroups, each walking its share in a
 // grid-stride loop. Fewer, longer-lived workgroups stream better than the
