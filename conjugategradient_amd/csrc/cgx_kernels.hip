@@ -1163,7 +1163,12 @@ __device__ __forceinline__ void sellp_slice2(const CsrArgs &A, const Gather &x, 
   const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
   const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
   epi.pre2(rc0, rc1);
-  const unsigned m0 = smask[r0], m1 = smask[r0 + 1];  // rows past n: mask 0 (array padded)
+  // both rows' masks in one load (r0 even; rows past n: mask 0, array padded)
+  using MT2 = typename std::conditional<(V & 16384) != 0, unsigned long long,
+                                        unsigned short>::type;
+  const MT2 mm = *reinterpret_cast<const MT2 *>(smask + r0);
+  constexpr int MB = 8 * (int)sizeof(MT);
+  const unsigned m0 = (unsigned)(mm & ((MT2(1) << (MB - 1) << 1) - 1)), m1 = (unsigned)(mm >> MB);
   const int nxm2 = (int)A.nx - 2;
   T acc0 = T(0), acc1 = T(0);
   for (int c = 0; c < W; c += 8) {
@@ -1253,18 +1258,29 @@ template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
     acc += s * pv;
   }
   __device__ __forceinline__ void pre2(int i0, int i1) {
-    pv = p[i0];
-    pv1 = p[i1];
+    using PV = typename PairOf<T>::V;
+    if (i1 == i0 + 1 && (((uintptr_t)(p + i0)) & (sizeof(PV) - 1)) == 0) {  // one pair load
+      const PV v = *reinterpret_cast<const PV *>(p + i0);
+      pv = v.x;
+      pv1 = v.y;
+    } else {
+      pv = p[i0];
+      pv1 = p[i1];
+    }
   }
   __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
-    if (l0) {
-      Ap[i] = s0;
-      acc += s0 * pv;
+    using PV = typename PairOf<T>::V;
+    if (l0 && l1 && (((uintptr_t)(Ap + i)) & (sizeof(PV) - 1)) == 0) {  // one pair store
+      PV v;
+      v.x = s0;
+      v.y = s1;
+      *reinterpret_cast<PV *>(Ap + i) = v;
+    } else {
+      if (l0) Ap[i] = s0;
+      if (l1) Ap[i + 1] = s1;
     }
-    if (l1) {
-      Ap[i + 1] = s1;
-      acc += s1 * pv1;
-    }
+    if (l0) acc += s0 * pv;
+    if (l1) acc += s1 * pv1;
   }
 };
 template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
