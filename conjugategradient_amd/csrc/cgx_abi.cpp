@@ -1125,9 +1125,15 @@ int autotune_spmv(cgx_csr *A) {
   }
   // (the software-pipelined SELL forms, 2056/2058, measured slower than the
   // plain ones on MI355X: profiles/r01_tune_sell.log; reachable by request)
-  std::vector<int> cands = {13, 15};
+  // A matrix stream far beyond the 256 MB Infinity Cache is never re-read
+  // from it, and inside the CG loop its non-temporal form keeps p and the
+  // vectors the other kernels hand over cached: 512^3 ran 305 it/s with nt
+  // against 281 with default-policy loads, a choice the isolated timing below
+  // cannot see (it ran both within 1%). Such matrices tune the format only.
+  const bool big = bytes > (int64_t(512) << 20);
+  std::vector<int> cands = big ? std::vector<int>{15} : std::vector<int>{13, 15};
   if (A->dev.sl) {
-    cands.push_back(2048);
+    if (!big) cands.push_back(2048);
     cands.push_back(2050);
   }
   cgx_ctx *ctx = A->ctx;
