@@ -153,7 +153,9 @@ class Matrix:
         return m
 
     def _drop_schedule(self):
-        if self._csr:
+        # a closed queue has already released the context the handle points
+        # into (interpreter shutdown, or a fixture closing the queue first)
+        if self._csr and self._queue.handle:
             lib().cgx_csr_destroy(self._csr)
         self._csr = None
 
@@ -403,7 +405,7 @@ class CG:
 
     # -- solve ----------------------------------------------------------
     def _drop_solver(self):
-        if self._cg:
+        if self._cg and self._queue.handle:  # see Matrix._drop_schedule
             lib().cgx_cg_destroy(self._cg)
         self._cg = None
         self._cg_for = None
