@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -569,6 +570,7 @@ extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
 
 int autotune_spmv(cgx_csr *A);
 int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
+int build_value_codes(cgx_csr *A);
 void free_sell(cgx_csr *A);
 
 // ===========================================================================
@@ -695,7 +697,8 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 
 void free_sell(cgx_csr *A) {
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
-                   &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask}) {
+                   &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask, &A->d_sell_vc,
+                   &A->d_sell_vdict}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -707,6 +710,9 @@ void free_sell(cgx_csr *A) {
   A->dev.sorder = nullptr;
   A->dev.sell_kind = 0;
   A->dev.smask = nullptr;
+  A->dev.svc = nullptr;
+  A->dev.svdict = nullptr;
+  A->dev.nvdict = 0;
   A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
@@ -801,7 +807,7 @@ static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
   pool.clear();
   std::vector<std::pair<std::vector<int>, int>> seen;
   std::vector<int> P;
-  int64_t voff = 0, padded = 0;
+  int64_t voff = 0, coff = 0, padded = 0;
   maxw = 0;
   for (int64_t q = 0; q < nsl; ++q) {
     const int64_t r0 = q * H, r1 = std::min(n, r0 + H);
@@ -831,8 +837,9 @@ static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
       if (seen.size() >= 16) seen.erase(seen.begin());
       seen.emplace_back(P, base);
     }
-    sl[(size_t)q] = SellSlice{voff, 0, base, W};
+    sl[(size_t)q] = SellSlice{voff, coff, base, W};  // coff: value-code chunks (16 B)
     voff += H * W;
+    coff += kSellRows * ((W + 7) / 8);
     padded += (r1 - r0) * W;
     maxw = std::max(maxw, W);
   }
@@ -935,6 +942,103 @@ static std::vector<int> sell_visit_order(int64_t nsl, int64_t H, int64_t P) {
     for (size_t i = 0; i < key.size(); ++i) order[(size_t)lo + i] = std::get<3>(key[i]);
   }
   return order;
+}
+
+// Value codes of A's SELL-P copy (cgx_internal.h kVcMax): the
+// dictionary starts from the distinct values of an evenly spread sample of
+// the value array; the pack kernel reports values it lacks, which join the
+// dictionary for another pass, until every value is found or there are more
+// than kVcMax of them (then the matrix keeps plain SELL-P values; not an
+// error). Errors are device failures only.
+template <typename T> static int build_value_codes_t(cgx_csr *A) {
+  using B = typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type;
+  cgx_ctx *ctx = A->ctx;
+  hipStream_t s = ctx->stream;
+  const int64_t nnz = A->dev.nnz;
+  const T *val = (const T *)A->dev.val;
+  std::vector<B> dict;
+  auto add = [&](const T *v, size_t cnt) {
+    for (size_t i = 0; i < cnt; ++i) {
+      B b;
+      std::memcpy(&b, v + i, sizeof(B));
+      auto it = std::lower_bound(dict.begin(), dict.end(), b);
+      if (it == dict.end() || *it != b) {
+        if ((int)dict.size() == kVcMax) return false;
+        dict.insert(it, b);
+      }
+    }
+    return true;
+  };
+  {  // sample: 64 pieces of up to 1024 values
+    constexpr int64_t kPieces = 64, kPiece = 1024;
+    std::vector<T> h((size_t)std::min<int64_t>(nnz, kPieces * kPiece));
+    if ((int64_t)h.size() == nnz) {
+      CGX_HIP(hipMemcpyAsync(h.data(), val, h.size() * sizeof(T), hipMemcpyDeviceToHost, s));
+    } else {
+      for (int64_t q = 0; q < kPieces; ++q) {
+        const int64_t at = (nnz - kPiece) * q / (kPieces - 1);
+        CGX_HIP(hipMemcpyAsync(h.data() + q * kPiece, val + at, kPiece * sizeof(T),
+                               hipMemcpyDeviceToHost, s));
+      }
+    }
+    CGX_HIP(hipStreamSynchronize(s));
+    if (!add(h.data(), h.size())) return CGX_OK;
+  }
+  int64_t chunks = 0;
+  {
+    std::vector<SellSlice> last(1);
+    CGX_HIP(hipMemcpyAsync(last.data(), A->dev.sl + (A->dev.nsl - 1), sizeof(SellSlice),
+                           hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    chunks = last[0].ioff + kSellRows * ((last[0].width + 7) / 8);
+  }
+  void *codes = nullptr, *ddict = nullptr, *dmiss = nullptr;
+  hipError_t e = hipMalloc(&codes, (size_t)chunks * 16);
+  if (e == hipSuccess) e = hipMalloc(&ddict, kVcDict * sizeof(T));
+  if (e == hipSuccess) e = hipMalloc(&dmiss, sizeof(int) + kVcDict * sizeof(T) + 16);
+  bool ok = false;
+  for (int pass = 0; pass < 16 && e == hipSuccess; ++pass) {
+    std::vector<T> hd(kVcDict, T(0));
+    std::memcpy(hd.data(), dict.data(), dict.size() * sizeof(T));
+    e = hipMemcpyAsync(ddict, hd.data(), kVcDict * sizeof(T), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(dmiss, 0, sizeof(int), s);
+    if (e == hipSuccess)
+      e = Launch<T>::sellpv_pack(A->dev, val, (const T *)ddict, (int)dict.size(),
+                                 (unsigned char *)codes, (int *)dmiss,
+                                 (T *)((char *)dmiss + 16), s);
+    int nmiss = 0;
+    std::vector<T> mv(kVcDict);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(&nmiss, dmiss, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(mv.data(), (char *)dmiss + 16, kVcDict * sizeof(T),
+                         hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) break;
+    if (nmiss == 0) {
+      ok = true;
+      break;
+    }
+    if (!add(mv.data(), (size_t)std::min(nmiss, kVcDict))) break;
+  }
+  if (dmiss) (void)hipFree(dmiss);
+  if (e != hipSuccess || !ok) {
+    if (codes) (void)hipFree(codes);
+    if (ddict) (void)hipFree(ddict);
+    if (e != hipSuccess) return hip_fail(e, "cgx_csr_create(value codes)");
+    return CGX_OK;
+  }
+  A->d_sell_vc = codes;
+  A->d_sell_vdict = ddict;
+  A->dev.svc = codes;
+  A->dev.svdict = ddict;
+  A->dev.nvdict = (int)dict.size();
+  return CGX_OK;
+}
+
+int build_value_codes(cgx_csr *A) {
+  if (!A->dev.sl || !A->dev.sell_kind || A->dev.nsl < 1 || A->dev.nnz < 1) return CGX_OK;
+  return A->dtype == CGX_F32 ? build_value_codes_t<float>(A) : build_value_codes_t<double>(A);
 }
 
 // SELL copy of A on the device with R rows per lane (0: the default layout),
@@ -1061,6 +1165,10 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
     free_sell(A);
     return hip_fail(e, "cgx_csr_create(SELL pack)");
   }
+  if (kind) {
+    const char *env = std::getenv("CGX_VALUE_CODES");
+    if (!env || std::atoi(env) != 0) return build_value_codes(A);
+  }
   return CGX_OK;
 }
 
@@ -1081,6 +1189,12 @@ extern "C" int cgx_csr_set_sell(cgx_csr *A, int rows_per_lane) {
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_value_codes(cgx_csr *A, int *n_values) {
+  CGX_REQUIRE(A && n_values, CGX_EINVAL, "NULL argument");
+  *n_values = A->dev.svc ? A->dev.nvdict : 0;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
   if (has_sell) *has_sell = !A->dev.sl ? 0 : (A->dev.sell_kind ? 3 : A->dev.sell_r);
@@ -1091,7 +1205,8 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
 static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
                            68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
-                           267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578};
+                           267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
+                           34816, 34818, 40960, 40962};
   for (int k : ok)
     if (k == v) return true;
   return false;
@@ -1102,6 +1217,8 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
   CGX_REQUIRE(known_variant(variant), CGX_EINVAL, "unknown SpMV variant %d", variant);
   CGX_REQUIRE(!(variant & (2048 | 8192)) || A->dev.sl, CGX_EUNSUPPORTED,
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
+  CGX_REQUIRE(!(variant & 32768) || A->dev.svc, CGX_EUNSUPPORTED,
+              "variant %d needs SELL-P value codes, which this matrix does not have", variant);
   A->dev.variant = variant;
   return CGX_OK;
 }
@@ -1120,7 +1237,7 @@ int autotune_spmv(cgx_csr *A) {
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
   if (bytes < (int64_t(64) << 20)) {  // small: the size heuristic, SELL where built
-    if (A->dev.sl) A->dev.variant = 2048;
+    if (A->dev.sl) A->dev.variant = A->dev.svc ? (2048 | 32768) : 2048;
     return CGX_OK;
   }
   // (the software-pipelined SELL forms, 2056/2058, measured slower than the
@@ -1135,6 +1252,10 @@ int autotune_spmv(cgx_csr *A) {
   if (A->dev.sl) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
+  }
+  if (A->dev.svc) {  // SELL-P value codes: 1 B per slot instead of 8
+    if (!big) cands.push_back(2048 | 32768);
+    cands.push_back(2050 | 32768);
   }
   cgx_ctx *ctx = A->ctx;
   hipStream_t s = ctx->stream;

@@ -79,9 +79,20 @@ constexpr unsigned kSellPad = 0xff;
 constexpr int kSellPatMax = 32;   // SELL-P: offsets per slice pattern (u32 masks)
 constexpr int kSellDefaultR = 2;    // rows per lane of the SELL copy cgx_csr_create builds
                                     // (2: 16-byte loads, profiles/r01_tune_sell2.log)
+// SELL-P value codes ("value codes"): a matrix with at most
+// kVcMax distinct values (bit patterns) gets, beside the SELL-P values, one
+// code byte per slot: 16 bytes per lane per chunk of 8 slots (byte 2 j + r:
+// slot j of the lane's row r), chunks of a slice consecutive from
+// SellSlice.ioff (in 16-byte units); kVcAbsent marks an empty slot. The
+// kernel reads the dictionary into LDS; the stream is 1 B per slot
+// instead of 8 (+ the row mask, which the code replaces).
+constexpr int kVcMax = 255;
+constexpr int kVcDict = 256;  // dictionary slots (entries past nvdict: zero)
+constexpr unsigned kVcAbsent = 0xff;
+
 struct SellSlice {
   int64_t voff;  // first value of the slice (entries)
-  int64_t ioff;  // first index word of the slice
+  int64_t ioff;  // first index word of the slice (SELL-P: first 16-byte code chunk)
   int dict;      // first entry of the slice's offset dictionary
   int width;     // entries per row in this slice (longest row)
 };
@@ -111,6 +122,12 @@ struct CsrDev {
   int sell_kind = 0;
   const void *smask = nullptr;
   int64_t nx = 0;  // length of the gathered vector (n, + ghosts when partitioned)
+  // SELL-P value codes (variant bit 32768, null when the matrix has more
+  // than kVcMax distinct values): one byte per slot, index into svdict
+  // (kVcAbsent: the row has no entry in the slot); layout at SellSlice.ioff
+  const void *svc = nullptr;
+  const void *svdict = nullptr;  // kVcDict values of the matrix's type
+  int nvdict = 0;                // distinct values (0: no codes)
 };
 
 template <typename T> struct Launch {
@@ -169,6 +186,11 @@ template <typename T> struct Launch {
   static hipError_t sell_pack(const CsrDev &A, const T *val, T *sval, hipStream_t s);
   static hipError_t sellp_pack(const CsrDev &A, const T *val, T *sval, void *mask,
                                hipStream_t s);
+  // value codes of the SELL-P layout (dict: nd sorted bit patterns); *miss
+  // counts the values not in the dictionary, the first kVcDict of them
+  // stored at missv
+  static hipError_t sellpv_pack(const CsrDev &A, const T *val, const T *dict, int nd,
+                                unsigned char *codes, int *miss, T *missv, hipStream_t s);
 };
 
 // axpby modes

@@ -251,6 +251,8 @@ struct CsrArgs {
   int part_off;  // per launch: first partial slot of k_spmv_dot (split launches)
   const void *smask;  // SELL-P slot masks
   int64_t nx;         // gathered vector length
+  const void *svc;    // SELL-P value codes (variant bit 32768)
+  const void *svdict; // their dictionary (kVcDict entries)
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -912,6 +914,7 @@ __device__ __forceinline__ void spmv_waves(const CsrArgs &A, const T *__restrict
 // only): no gathers.
 // ---------------------------------------------------------------------------
 template <typename T> struct SellLds {
+  T vdict[kVcDict];  // value-code dictionary (variant bit 32768)
   T red[4 * kMaxRed];
   int flag;
   int rp[1];  // unused (keeps the SpmvLds member set)
@@ -1212,6 +1215,74 @@ __device__ __forceinline__ void spmv_sellp(const CsrArgs &A, const Gather &x, Ep
     sellp_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
 
+// SELL-P with value codes (variant bit 32768 | 8192): the SELL-P slice walk
+// and pair gathers, but each slot's value comes from a 1-byte code into the
+// matrix's value dictionary (in LDS) instead of an 8-byte value, and the
+// code also says whether the row has an entry there (kVcAbsent), so no mask
+// is read: the matrix stream is 8 B per row pair and chunk of 8 slots
+// instead of 128 + 2. Decoding returns the stored value's exact bits, so the
+// sums are the SELL-P sums, bit for bit.
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x, Epi &epi,
+                                              const T *__restrict__ vd, int s) {
+  constexpr bool NT = (V & 2) != 0;
+  const Ull2 *__restrict__ codes = static_cast<const Ull2 *>(A.svc);
+  const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
+  const auto *pat = (const __attribute__((address_space(4))) int *)A.sdict;
+  const int lane = threadIdx.x & 63;
+  const int si = __builtin_amdgcn_readfirstlane(s);
+  const int64_t coff = cs[si].ioff;
+  const int pbase = cs[si].dict, W = cs[si].width;
+  const int r0 = si * (2 * kSellRows) + 2 * lane;
+  const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
+  const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
+  epi.pre2(rc0, rc1);
+  const int nxm2 = (int)A.nx - 2;
+  T acc0 = T(0), acc1 = T(0);
+  for (int c = 0; c < W; c += 8) {
+    const Ull2 cw = ldg<NT>(codes + coff + (int64_t)(c >> 3) * kSellRows + lane);
+    T g0[8], g1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = pat[pbase + min(c + j, W - 1)];
+      const int base = r0 + o;
+      const int cb = min(max(base, 0), nxm2);
+      if constexpr ((V & 16) != 0) {
+        g0[j] = T(cb & 1);
+        g1[j] = T(cb & 2);
+      } else {
+        const auto g = x.pair(cb);
+        g0[j] = base <= nxm2 ? g.x : g.y;
+        g1[j] = base >= 0 ? g.y : g.x;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned long long w = j < 4 ? cw.x : cw.y;
+      const unsigned k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
+      const unsigned k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
+      const T t0 = acc0 + vd[k0] * g0[j];
+      const T t1 = acc1 + vd[k1] * g1[j];
+      acc0 = k0 != kVcAbsent ? t0 : acc0;
+      acc1 = k1 != kVcAbsent ? t1 : acc1;
+    }
+  }
+  epi.row2(r0, acc0, acc1, l0, l1);
+}
+
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, Epi &epi,
+                                            T *vd) {
+  const T *__restrict__ src = static_cast<const T *>(A.svdict);
+  for (int i = threadIdx.x; i < kVcDict; i += kBlock) vd[i] = src[i];
+  __syncthreads();
+  int s, step, end, lo;
+  sell_range((int)A.nsl, s, step, end, lo);
+  for (; s < end; s += step)
+    sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd,
+                                     slice_at(A, A.rev ? lo + end - 1 - s : s));
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
@@ -1222,7 +1293,8 @@ using LdsOf = typename std::conditional<
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
                                          const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
-  if constexpr ((V & 8192) != 0) spmv_sellp<T, V, Epi, Gather>(A, x, epi);
+  if constexpr ((V & 32768) != 0) spmv_sellpv<T, V, Epi, Gather>(A, x, epi, sm.vdict);
+  else if constexpr ((V & 8192) != 0) spmv_sellp<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0) spmv_sell<T, V, Epi, Gather>(A, x, epi);
@@ -1786,6 +1858,58 @@ __global__ __launch_bounds__(kBlock) void k_sellp_pack(int64_t n, int64_t nsl,
   }
 }
 
+// SELL-P value codes: the slot layout of k_sellp_pack, each stored value
+// replaced by its index in the sorted dictionary `dict` of nd bit patterns
+// (binary search on the bits: -0.0 / 0.0 and NaN payloads stay distinct);
+// empty slots and rows past n: kVcAbsent. A value not in the dictionary
+// counts in *miss and the first kVcDict of them land in missv (the host adds
+// them to the dictionary and packs again, or drops the codes).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sellpv_pack(int64_t n, int64_t nsl,
+                                                        const int *__restrict__ rowptr,
+                                                        const int *__restrict__ col,
+                                                        const T *__restrict__ val,
+                                                        const SellSlice *__restrict__ sl,
+                                                        const int *__restrict__ pat,
+                                                        const T *__restrict__ dict, int nd,
+                                                        unsigned char *__restrict__ codes,
+                                                        int *miss, T *missv) {
+  using B = typename Bits<T>::U;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t H = 2 * kSellRows;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nsl * H; i += stride) {
+    const SellSlice m = sl[i / H];
+    const int li = (int)(i % H), l = li >> 1, r = li & 1;
+    const int *P = pat + m.dict;
+    int a = 0, e = 0;
+    if (i < n) {
+      a = rowptr[i];
+      e = rowptr[i + 1];
+    }
+    int k = a;
+    const int W8 = (m.width + 7) & ~7;
+    for (int j = 0; j < W8; ++j) {
+      unsigned code = kVcAbsent;
+      if (j < m.width && k < e && col[k] - (int)i == P[j]) {
+        const B vb = __builtin_bit_cast(B, val[k++]);
+        int lo = 0, hi = nd;  // first dictionary entry >= vb
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (__builtin_bit_cast(B, dict[mid]) < vb) lo = mid + 1;
+          else hi = mid;
+        }
+        if (lo < nd && __builtin_bit_cast(B, dict[lo]) == vb) code = (unsigned)lo;
+        else {
+          const int q = atomicAdd(miss, 1);
+          if (q < kVcDict) missv[q] = val[k - 1];
+        }
+      }
+      codes[(m.ioff + (int64_t)(j >> 3) * kSellRows + l) * 16 + 2 * (j & 7) + r] =
+          (unsigned char)code;
+    }
+  }
+}
+
 // Poisson rows [row_begin, row_end): columns ascending (-z,-y,-x,d,+x,+y,+z).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_poisson(int dim, int nx, int ny, int nz,
@@ -1827,7 +1951,7 @@ inline int elem_grid(int64_t n, int per_thread) {
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
                  A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
-                 A.smask,  A.nx > 0 ? A.nx : A.n};
+                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict};
 }
 
 }  // namespace
@@ -2044,6 +2168,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   if (v >= 0 && (v & (2048 | 8192))) {
     // the variant follows the SELL copy's layout: bit 4096 for 2 rows per
     // lane; pipelined (bit 8) for 1 row per lane and slices <= 8 wide
+    if (A.sl && A.sell_kind && (v & 32768) && A.svc) return 32768 | 8192 | (v & (16 | 2));
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2121,6 +2246,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 8194: CGX_LAUNCH_V(KERNEL, 8194, __VA_ARGS__);                               \
     case 24576: CGX_LAUNCH_V(KERNEL, 24576, __VA_ARGS__);                             \
     case 24578: CGX_LAUNCH_V(KERNEL, 24578, __VA_ARGS__);                             \
+    case 40960: CGX_LAUNCH_V(KERNEL, 40960, __VA_ARGS__);                             \
+    case 40962: CGX_LAUNCH_V(KERNEL, 40962, __VA_ARGS__);                             \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -2181,6 +2308,7 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 6160: CGX_LAUNCH_V(k_spmv_dot, 6160, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 6162: CGX_LAUNCH_V(k_spmv_dot, 6162, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 8210: CGX_LAUNCH_V(k_spmv_dot, 8210, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 40978: CGX_LAUNCH_V(k_spmv_dot, 40978, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -2310,6 +2438,15 @@ hipError_t Launch<T>::sellp_pack(const CsrDev &A, const T *val, T *sval, void *m
   else
     hipLaunchKernelGGL((k_sellp_pack<T, unsigned char>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
                        A.rowptr, A.col, val, A.sl, A.sdict, sval, (unsigned char *)mask);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t Launch<T>::sellpv_pack(const CsrDev &A, const T *val, const T *dict, int nd,
+                                  unsigned char *codes, int *miss, T *missv, hipStream_t s) {
+  const int g = elem_grid(A.nsl * kSellRows * 2, 4);
+  hipLaunchKernelGGL(k_sellpv_pack<T>, dim3(g), dim3(kBlock), 0, s, A.n, A.nsl, A.rowptr, A.col,
+                     val, A.sl, A.sdict, dict, nd, codes, miss, missv);
   return hipGetLastError();
 }
 

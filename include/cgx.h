@@ -94,6 +94,11 @@ int cgx_csr_set_sell(cgx_csr *csr, int rows_per_lane);
 /* The matrix's SELL layout (0 none, 1 / 2 dictionary SELL with that many
  * rows per lane, 3 SELL-P) and its padded entry count. */
 int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
+/* Distinct values of the matrix's SELL-P value codes (variant bit 32768:
+ * one code byte per slot into a dictionary of at most 255 values, built by
+ * cgx_csr_create when the SELL-P copy exists and the matrix has that few
+ * distinct values; $CGX_VALUE_CODES=0 disables it), 0 when it has none. */
+int cgx_csr_value_codes(cgx_csr *csr, int *n_values);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
  * Scalars are DEVICE pointers, as in the reference (Scalar<DT>::ptr()). */
@@ -242,7 +247,8 @@ int cgx_mm_write_lower(const char *path, int64_t n, const int *rowptr, const int
                        const double *val, int threads);
 
 /* Host-only: the SELL-P layout (2 rows per lane, slices of 128 rows): per
- * slice {first value slot, 0, first pattern entry, pattern width}; pat[npat]
+ * slice {first value slot, first 16-byte value-code chunk, first pattern
+ * entry, pattern width}; pat[npat]
  * the sorted (col - row) patterns. *nsl = 0 when the matrix does not
  * qualify (a pattern wider than 32, unsorted rows, too much padding). */
 int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,

@@ -1,0 +1,165 @@
+"""SELL-P value codes (variant bit 32768) against the oracle.
+
+A matrix with a SELL-P copy and at most 255 distinct values (bit patterns)
+also gets one code byte per slot into a value dictionary; the kernel decodes
+the stored value's exact bits, so the bar is bit-exactness with the oracle's
+restatement of the reference SpMV (VectorOperations.hpp:438-466) and with the
+plain SELL-P variant. Matrices with more distinct values keep plain values.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import conjugategradient_amd as cga
+from conjugategradient_amd import Matrix, Vector, VectorOperations
+from conjugategradient_amd._native import CgxError, check, lib
+from tests.test_gpu_sell import banded
+from tests.util import rel
+
+pytestmark = pytest.mark.gpu
+
+VC = [34816, 34818]          # SELL-P with value codes: default / non-temporal loads
+PLAIN = [8192, 8194, 13]     # SELL-P values, CSR-stream
+
+
+def quantized_banded(n, levels, seed=5, rare=0):
+    """banded() with values snapped to `levels` distinct numbers; `rare` > 0
+    gives rows in the middle of the matrix values of their own (absent from
+    the host's spread sample: the pack kernel's miss path adds them)."""
+    rp, cl, vl = banded(n, half=4, seed=seed)
+    grid = np.linspace(vl.min(), vl.max(), levels)
+    vl = grid[np.clip(np.searchsorted(grid, vl), 0, levels - 1)]
+    if rare:
+        mid = n // 2 + 17
+        for t in range(rare):
+            vl[rp[mid + 3 * t]] = 1000.0 + t / 7.0
+    return rp, cl, vl
+
+
+def n_codes(m):
+    nv = C.c_int()
+    check(lib().cgx_csr_value_codes(m.schedule(), C.byref(nv)))
+    return nv.value
+
+
+def spmv_all(queue, A, x, variants, dtype=np.float64):
+    n = A.N()
+    ops = VectorOperations(queue, dtype)
+    ops.setVectorSize(n)
+    xv = Vector(queue, x, dtype=dtype)
+    out = {}
+    for v in variants:
+        check(lib().cgx_csr_set_variant(A.schedule(), v))
+        yv = Vector(queue, n, dtype=dtype)
+        ops.spmv(A, xv, yv, A.NNZ(), count=n)
+        out[v] = yv.to_numpy()
+    return out
+
+
+CASES = {
+    "poisson2d": lambda O: O.poisson(2, 96, 80, 1),
+    "poisson3d_ragged": lambda O: O.poisson(3, 23, 19, 17),
+    "poisson3d_64": lambda O: O.poisson(3, 64, 64, 64),        # > sample size
+    "quant200": lambda O: quantized_banded(60_001, 200),
+    "quant_rare": lambda O: quantized_banded(60_001, 40, rare=20),
+    "tiny": lambda O: (np.array([0, 1, 3, 4], np.int32), np.array([0, 0, 1, 2], np.int32),
+                       np.array([2.0, -1.0, 3.0, 4.0])),
+}
+EXPECT_CODES = {"poisson2d": 2, "poisson3d_ragged": 2, "poisson3d_64": 2, "tiny": 4,
+                "quant_rare": None, "quant200": None}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_value_codes_bitexact(queue, oracle, case, dtype):
+    rp, cl, vl = CASES[case](oracle)
+    n = len(rp) - 1
+    A = Matrix(queue, vl, cl, rp, dtype=dtype)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    nv = n_codes(A)
+    distinct = len(np.unique(vl.astype(dtype).view(np.uint64 if dtype == np.float64
+                                                   else np.uint32)))
+    assert nv == distinct, (case, nv, distinct)
+    if EXPECT_CODES[case] is not None:
+        assert nv == EXPECT_CODES[case]
+    x = np.random.default_rng(3).standard_normal(n)
+    out = spmv_all(queue, A, x, VC + PLAIN, dtype)
+    v = C.c_int()
+    check(lib().cgx_csr_set_variant(A.schedule(), 34818))
+    check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
+    assert v.value == 40962
+    ref = oracle.spmv(rp, cl, vl, x) if dtype == np.float64 else out[8192]
+    for k in VC + PLAIN:
+        np.testing.assert_array_equal(out[k], ref, err_msg=f"variant {k}")
+
+
+def test_value_codes_refused_past_255_values(queue, oracle):
+    rp, cl, vl = quantized_banded(20_011, 2000)
+    assert len(np.unique(vl)) > 255
+    A = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    assert n_codes(A) == 0
+    with pytest.raises(CgxError, match="value codes"):
+        check(lib().cgx_csr_set_variant(A.schedule(), 34816))
+    # plain SELL-P still works
+    x = np.random.default_rng(1).standard_normal(len(rp) - 1)
+    np.testing.assert_array_equal(spmv_all(queue, A, x, [8192])[8192],
+                                  oracle.spmv(rp, cl, vl, x))
+
+
+def test_value_codes_disabled_by_env(queue, oracle, monkeypatch):
+    monkeypatch.setenv("CGX_VALUE_CODES", "0")
+    rp, cl, vl = oracle.poisson(2, 40, 40, 1)
+    A = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    assert n_codes(A) == 0
+
+
+def test_value_codes_signed_zero_and_nonfinite(queue, oracle):
+    # -0.0 and +0.0 are distinct dictionary entries (bit patterns); a stored
+    # 0 times an Inf in x is NaN as in the reference, an empty slot is not
+    rp, cl, vl = oracle.poisson(2, 16, 12, 1)
+    vl = vl.copy()
+    vl[3] = -0.0
+    vl[10] = 0.0
+    vl[11] = np.nan
+    n = len(rp) - 1
+    x = np.random.default_rng(7).standard_normal(n)
+    x[5] = np.inf
+    x[40] = -0.0
+    A = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    assert n_codes(A) == 5
+    y = spmv_all(queue, A, x, VC)
+    ref = oracle.spmv(rp, cl, vl, x)
+    for k in VC:
+        np.testing.assert_array_equal(np.isnan(y[k]), np.isnan(ref))
+        ok = ~np.isnan(ref)
+        np.testing.assert_array_equal(y[k][ok], ref[ok])
+        np.testing.assert_array_equal(np.signbit(y[k][ok]), np.signbit(ref[ok]))
+
+
+@pytest.mark.parametrize("dim,n", [(2, 64), (3, 24)])
+def test_cg_with_value_codes_matches_plain(oracle, monkeypatch, dim, n):
+    """CG through the default path (autotune may pick value codes; small
+    matrices take them by the size rule) equals the run with codes disabled
+    bit for bit, and the oracle within the SURVEY §8(c) tolerances."""
+    rp, cl, vl = oracle.poisson(dim, n, n, n)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    xs = {}
+    for vc in ("1", "0"):
+        monkeypatch.setenv("CGX_VALUE_CODES", vc)
+        cg = cga.CG.createCG()
+        cg.setMatrix(vl, cl, rp)
+        cg.setTarget(b)
+        cg.solve(1e-8)
+        v = C.c_int()
+        check(lib().cgx_csr_variant(cg.A.schedule(), C.byref(v)))
+        assert bool(v.value & 32768) == (vc == "1")
+        xs[vc] = (cg.extract(), cg.iterations)
+    np.testing.assert_array_equal(xs["1"][0], xs["0"][0])
+    assert xs["1"][1] == xs["0"][1]
+    xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-8)
+    assert abs(xs["1"][1] - res.iterations) <= 2
+    assert rel(xs["1"][0], xr) <= 1e-10
