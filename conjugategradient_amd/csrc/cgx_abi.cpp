@@ -165,7 +165,7 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
   if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & 2048)) {
     bool async = false;
     if ((rc = dist_halo_post(A, p, s, &async))) return rc;
-    const int gi = Launch<T>::slice_grid(A->split_ni);
+    const int gi = Launch<T>::slice_grid(A->dev, A->split_ni);
     // one timed region: interior slices, the wait for the halo, boundary slices
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap,
@@ -177,7 +177,7 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            return e;
          })))
       return rc;
-    *np = gi + Launch<T>::slice_grid(A->split_nb);
+    *np = gi + Launch<T>::slice_grid(A->dev, A->split_nb);
     return CGX_OK;
   }
   if (halo && (rc = dist_halo_exchange(A, p, s))) return rc;

@@ -153,7 +153,7 @@ template <typename T> struct Launch {
   static hipError_t spmv_dot_slices(const CsrDev &A, const int *list, int count, int part_off,
                                     const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
                                     hipStream_t s, int rev = 0);
-  static int slice_grid(int count);
+  static int slice_grid(const CsrDev &A, int count);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);

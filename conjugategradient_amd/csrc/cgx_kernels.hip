@@ -29,6 +29,9 @@
 //    as in the reference's expressions.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include <cstdlib>
 #include <type_traits>
 
@@ -1239,32 +1242,41 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
   epi.pre2(rc0, rc1);
   const int nxm2 = (int)A.nx - 2;
   T acc0 = T(0), acc1 = T(0);
+  // bit 131072: gather and sum the chunk in two halves of 4 slots (half the
+  // registers in flight)
+  constexpr int HS = (V & 131072) ? 4 : 8;
   for (int c = 0; c < W; c += 8) {
     const Ull2 cw = ldg<NT>(codes + coff + (int64_t)(c >> 3) * kSellRows + lane);
-    T g0[8], g1[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int h = 0; h < 8; h += HS) {
+    T g0[HS], g1[HS];
+#pragma unroll
+    for (int jj = 0; jj < HS; ++jj) {
+      const int j = h + jj;
       const int o = pat[pbase + min(c + j, W - 1)];
       const int base = r0 + o;
       const int cb = min(max(base, 0), nxm2);
       if constexpr ((V & 16) != 0) {
-        g0[j] = T(cb & 1);
-        g1[j] = T(cb & 2);
+        g0[jj] = T(cb & 1);
+        g1[jj] = T(cb & 2);
       } else {
         const auto g = x.pair(cb);
-        g0[j] = base <= nxm2 ? g.x : g.y;
-        g1[j] = base >= 0 ? g.y : g.x;
+        g0[jj] = base <= nxm2 ? g.x : g.y;
+        g1[jj] = base >= 0 ? g.y : g.x;
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int jj = 0; jj < HS; ++jj) {
+      const int j = h + jj;
       const unsigned long long w = j < 4 ? cw.x : cw.y;
       const unsigned k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
       const unsigned k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
-      const T t0 = acc0 + vd[k0] * g0[j];
-      const T t1 = acc1 + vd[k1] * g1[j];
+      const T t0 = acc0 + vd[k0] * g0[jj];
+      const T t1 = acc1 + vd[k1] * g1[jj];
       acc0 = k0 != kVcAbsent ? t0 : acc0;
       acc1 = k1 != kVcAbsent ? t1 : acc1;
+    }
+    if constexpr (HS < 8) __builtin_amdgcn_sched_barrier(0);
     }
   }
   epi.row2(r0, acc0, acc1, l0, l1);
@@ -1482,8 +1494,16 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
   }
 }
 
+// Waves per SIMD a SpMV kernel asks the register allocator for: the
+// value-code SELL-P form needs 8 (its persistent grid of kMaxGrid workgroups
+// is then resident at once); the rest take what they get.
+template <int V> struct SpmvWaves {
+  static constexpr int w = (V & 32768) && (V & (65536 | 131072)) ? 8 : 1;
+};
+
 template <typename T, int V>
-__global__ __launch_bounds__(kBlock) void k_spmv_dot(CsrArgs A, const T *__restrict__ val,
+__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
+                                                                      const T *__restrict__ val,
                                                      const T *__restrict__ p,
                                                      T *__restrict__ Ap, CgScalars<T> *st,
                                                      int slot, RedWs<T> *ws) {
@@ -2168,7 +2188,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   if (v >= 0 && (v & (2048 | 8192))) {
     // the variant follows the SELL copy's layout: bit 4096 for 2 rows per
     // lane; pipelined (bit 8) for 1 row per lane and slices <= 8 wide
-    if (A.sl && A.sell_kind && (v & 32768) && A.svc) return 32768 | 8192 | (v & (16 | 2));
+    if (A.sl && A.sell_kind && (v & 32768) && A.svc)
+      return 32768 | 8192 | (v & (16 | 2 | 65536 | 131072));
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2251,6 +2272,57 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     default: return hipErrorInvalidValue;                                      \
   }
 
+// Workgroups of k_spmv_dot<T, v> resident on the device at once (occupancy
+// x CUs; 0: unknown variant). The SpMV grid is capped to it: a persistent
+// grid larger than what fits runs its last workgroups as a second wave,
+// after the first ones finish their fixed shares, and that tail measured
+// 8% of the value-code kernel at 256^3 (tools/gpu_vc_ab.sh). $CGX_SPMV_RESIDENT=0
+// turns the cap off (A/B).
+#define CGX_SPMV_LIST(X)                                                              \
+  X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(64) X(65) X(66)   \
+  X(67) X(68) X(69) X(70) X(71) X(524) X(525) X(526) X(527) X(264) X(265) X(266)      \
+  X(267) X(140) X(141) X(142) X(143) X(76) X(77) X(78) X(79) X(2048) X(2050) X(2056)  \
+  X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)        \
+  X(40978) X(106498) X(172034)
+template <typename T> const void *spmv_dot_kernel(int v) {
+  switch (v) {
+#define CGX_KP(VV) \
+  case VV: return reinterpret_cast<const void *>(&k_spmv_dot<T, VV>);
+    CGX_SPMV_LIST(CGX_KP)
+#undef CGX_KP
+    default: return nullptr;
+  }
+}
+
+template <typename T> int spmv_dot_resident(int v) {
+  static const bool on = [] {
+    const char *e = std::getenv("CGX_SPMV_RESIDENT");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (!on) return 0;
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;  // (device, variant) -> workgroups
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, v});
+  if (it != cache.end()) return it->second;
+  int res = 0;
+  if (const void *k = spmv_dot_kernel<T>(v)) {
+    int nb = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      res = nb * cus;
+  }
+  cache[{dev, v}] = res;
+  return res;
+}
+
+template <typename T> static int cap_resident(int grid, int v) {
+  const int r = spmv_dot_resident<T>(v);
+  return (r > 0 && r < grid) ? r : grid;
+}
+
 template <typename T>
 hipError_t Launch<T>::spmv(const CsrDev &A, const T *x, T *y, hipStream_t s) {
   const int spmv_grid_ = grid_rows(A.nrb);
@@ -2269,8 +2341,9 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
                                int slot, RedWs<T> *ws, hipStream_t s, int rev) {
   CsrArgs a = args(A);
   a.rev = rev;
-  const int spmv_grid_ = grid_rows(A.nrb);
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
+  const int v = spmv_variant<T>(A);
+  const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), v);
+  CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
 }
 // SpMV + p.Ap over a list of SELL slices (a partitioned matrix's interior or
 // boundary slices), its partials at [part_off, part_off + grid)
@@ -2285,18 +2358,18 @@ hipError_t Launch<T>::spmv_dot_slices(const CsrDev &A, const int *list, int coun
   a.nsl = count;
   a.part_off = part_off;
   a.rev = rev;
-  const int spmv_grid_ = slice_grid(count);
+  const int spmv_grid_ = slice_grid(A, count);
   CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
 }
-template <typename T> int Launch<T>::slice_grid(int count) {
+template <typename T> int Launch<T>::slice_grid(const CsrDev &A, int count) {
   const int g = (count + 3) / 4;  // one wave per slice, 4 waves per workgroup
-  return g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g);
+  return cap_resident<T>(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g), spmv_variant<T>(A));
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                        CgScalars<T> *st, RedWs<T> *ws, hipStream_t s) {
   const int vv = spmv_variant<T>(A, v);
-  const int spmv_grid_ = grid_rows(A.nrb);
+  const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), vv);
   switch (vv) {  // timing ablations (bits 16/32) exist for this kernel only
     case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -2309,6 +2382,8 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 6162: CGX_LAUNCH_V(k_spmv_dot, 6162, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 8210: CGX_LAUNCH_V(k_spmv_dot, 8210, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 40978: CGX_LAUNCH_V(k_spmv_dot, 40978, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 106498: CGX_LAUNCH_V(k_spmv_dot, 106498, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 172034: CGX_LAUNCH_V(k_spmv_dot, 172034, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -2328,7 +2403,9 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
   }
   return hipGetLastError();
 }
-template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) { return grid_rows(A.nrb); }
+template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
+  return cap_resident<T>(grid_rows(A.nrb), spmv_variant<T>(A));  // = spmv_dot's grid
+}
 template <typename T> int Launch<T>::update_parts(int64_t n) {
   return grid_elems(n, kGridUpdateR);  // k_update_r's grid: one r.r partial per workgroup
 }
