@@ -698,7 +698,7 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 void free_sell(cgx_csr *A) {
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
                    &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask, &A->d_sell_vc,
-                   &A->d_sell_vdict}) {
+                   &A->d_sell_vdict, &A->d_sell_vc4}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -713,6 +713,7 @@ void free_sell(cgx_csr *A) {
   A->dev.svc = nullptr;
   A->dev.svdict = nullptr;
   A->dev.nvdict = 0;
+  A->dev.svc4 = nullptr;
   A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
@@ -1033,6 +1034,18 @@ template <typename T> static int build_value_codes_t(cgx_csr *A) {
   A->dev.svc = codes;
   A->dev.svdict = ddict;
   A->dev.nvdict = (int)dict.size();
+  if ((int)dict.size() <= kVc4Max) {  // 4-bit codes: half the code stream
+    void *c4 = nullptr;
+    e = hipMalloc(&c4, (size_t)chunks * 8);
+    if (e == hipSuccess) e = Launch<T>::vc_narrow(codes, c4, chunks, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      if (c4) (void)hipFree(c4);
+      return hip_fail(e, "cgx_csr_create(4-bit value codes)");
+    }
+    A->d_sell_vc4 = c4;
+    A->dev.svc4 = c4;
+  }
   return CGX_OK;
 }
 
@@ -1206,7 +1219,8 @@ static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
                            68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
-                           34816, 34818, 40960, 40962};
+                           34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
+                           821248, 821250};
   for (int k : ok)
     if (k == v) return true;
   return false;
@@ -1219,6 +1233,8 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
   CGX_REQUIRE(!(variant & 32768) || A->dev.svc, CGX_EUNSUPPORTED,
               "variant %d needs SELL-P value codes, which this matrix does not have", variant);
+  CGX_REQUIRE(!(variant & 262144) || A->dev.svc4, CGX_EUNSUPPORTED,
+              "variant %d needs 4-bit value codes (at most 15 distinct values)", variant);
   A->dev.variant = variant;
   return CGX_OK;
 }
@@ -1237,7 +1253,9 @@ int autotune_spmv(cgx_csr *A) {
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
   if (bytes < (int64_t(64) << 20)) {  // small: the size heuristic, SELL where built
-    if (A->dev.sl) A->dev.variant = A->dev.svc ? (2048 | 32768) : 2048;
+    if (A->dev.sl)
+      A->dev.variant = (A->dev.svc4 ? (2048 | 32768 | 262144) : A->dev.svc ? (2048 | 32768) : 2048) |
+                       (A->dev.svc && A->dev.sell_maxw <= 8 ? 524288 : 0);
     return CGX_OK;
   }
   // (the software-pipelined SELL forms, 2056/2058, measured slower than the
@@ -1253,9 +1271,15 @@ int autotune_spmv(cgx_csr *A) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
   }
-  if (A->dev.svc) {  // SELL-P value codes: 1 B per slot instead of 8
-    if (!big) cands.push_back(2048 | 32768);
-    cands.push_back(2050 | 32768);
+  // SELL-P value codes: 1 B per slot instead of 8 (4-bit codes: 0.5 B), and
+  // their software-pipelined loop (bit 524288) where no slice is over 8 wide
+  for (int c4 : {0, 262144}) {
+    if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
+    for (int pipe : {0, 524288}) {
+      if (pipe && A->dev.sell_maxw > 8) continue;
+      if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
+      cands.push_back(2050 | 32768 | c4 | pipe);
+    }
   }
   cgx_ctx *ctx = A->ctx;
   hipStream_t s = ctx->stream;

@@ -89,6 +89,7 @@ constexpr int kSellDefaultR = 2;    // rows per lane of the SELL copy cgx_csr_cr
 constexpr int kVcMax = 255;
 constexpr int kVcDict = 256;  // dictionary slots (entries past nvdict: zero)
 constexpr unsigned kVcAbsent = 0xff;
+constexpr int kVc4Max = 15;  // 4-bit codes: 15 values, 0xf empty
 
 struct SellSlice {
   int64_t voff;  // first value of the slice (entries)
@@ -128,6 +129,9 @@ struct CsrDev {
   const void *svc = nullptr;
   const void *svdict = nullptr;  // kVcDict values of the matrix's type
   int nvdict = 0;                // distinct values (0: no codes)
+  // 4-bit codes (variant bit 262144; at most kVc4Max values): 8 bytes per
+  // lane per chunk, byte j = slot j, row 0 in the low nibble
+  const void *svc4 = nullptr;
 };
 
 template <typename T> struct Launch {
@@ -191,6 +195,8 @@ template <typename T> struct Launch {
   // stored at missv
   static hipError_t sellpv_pack(const CsrDev &A, const T *val, const T *dict, int nd,
                                 unsigned char *codes, int *miss, T *missv, hipStream_t s);
+  // 8-bit codes (chunks x 16 B) -> 4-bit codes (chunks x 8 B)
+  static hipError_t vc_narrow(const void *codes8, void *codes4, int64_t chunks, hipStream_t s);
 };
 
 // axpby modes

@@ -256,6 +256,7 @@ struct CsrArgs {
   int64_t nx;         // gathered vector length
   const void *svc;    // SELL-P value codes (variant bit 32768)
   const void *svdict; // their dictionary (kVcDict entries)
+  const void *svc4;   // 4-bit value codes (variant bit 262144)
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -1245,8 +1246,17 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
   // bit 131072: gather and sum the chunk in two halves of 4 slots (half the
   // registers in flight)
   constexpr int HS = (V & 131072) ? 4 : 8;
+  constexpr bool C4 = (V & 262144) != 0;  // 4-bit codes: one 8-byte word per lane
+  const unsigned long long *__restrict__ codes4 =
+      static_cast<const unsigned long long *>(A.svc4);
   for (int c = 0; c < W; c += 8) {
-    const Ull2 cw = ldg<NT>(codes + coff + (int64_t)(c >> 3) * kSellRows + lane);
+    Ull2 cw;
+    if constexpr (C4) {
+      cw.x = ldg<NT>(codes4 + coff + (int64_t)(c >> 3) * kSellRows + lane);
+      cw.y = 0;
+    } else {
+      cw = ldg<NT>(codes + coff + (int64_t)(c >> 3) * kSellRows + lane);
+    }
 #pragma unroll
     for (int h = 0; h < 8; h += HS) {
     T g0[HS], g1[HS];
@@ -1268,18 +1278,132 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
 #pragma unroll
     for (int jj = 0; jj < HS; ++jj) {
       const int j = h + jj;
-      const unsigned long long w = j < 4 ? cw.x : cw.y;
-      const unsigned k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
-      const unsigned k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
+      unsigned k0, k1;
+      bool on0, on1;
+      if constexpr (C4) {
+        k0 = (unsigned)(cw.x >> (8 * j)) & 0xfu;
+        k1 = (unsigned)(cw.x >> (8 * j + 4)) & 0xfu;
+        on0 = k0 != 0xfu;
+        on1 = k1 != 0xfu;
+      } else {
+        const unsigned long long w = j < 4 ? cw.x : cw.y;
+        k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
+        k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
+        on0 = k0 != kVcAbsent;
+        on1 = k1 != kVcAbsent;
+      }
       const T t0 = acc0 + vd[k0] * g0[jj];
       const T t1 = acc1 + vd[k1] * g1[jj];
-      acc0 = k0 != kVcAbsent ? t0 : acc0;
-      acc1 = k1 != kVcAbsent ? t1 : acc1;
+      acc0 = on0 ? t0 : acc0;
+      acc1 = on1 ? t1 : acc1;
     }
     if constexpr (HS < 8) __builtin_amdgcn_sched_barrier(0);
     }
   }
   epi.row2(r0, acc0, acc1, l0, l1);
+}
+
+// Software-pipelined value-code SELL-P (variant bit 524288; every slice at
+// most 8 wide, i.e. one code chunk): while slice s gathers and sums, the
+// next slice's descriptor and offset pattern (a dependent pair of scalar
+// loads) and its code word are in flight, so a slice's critical path is its
+// own gathers. Same sums in the same order as sellpv_slice2.
+template <typename T, int V, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather &x, Epi &epi,
+                                                 const T *__restrict__ vd) {
+  constexpr bool NT = (V & 2) != 0;
+  constexpr bool C4 = (V & 262144) != 0;
+  const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
+  const auto *pat = (const __attribute__((address_space(4))) int *)A.sdict;
+  const Ull2 *__restrict__ codes = static_cast<const Ull2 *>(A.svc);
+  const unsigned long long *__restrict__ codes4 =
+      static_cast<const unsigned long long *>(A.svc4);
+  const int lane = threadIdx.x & 63;
+  const int nxm2 = (int)A.nx - 2;
+  int s, step, end, lo;
+  sell_range((int)A.nsl, s, step, end, lo);
+  if (s >= end) return;
+  auto code_at = [&](int64_t coff) {
+    Ull2 cw;
+    if constexpr (C4) {
+      cw.x = ldg<NT>(codes4 + coff + lane);
+      cw.y = 0;
+    } else {
+      cw = ldg<NT>(codes + coff + lane);
+    }
+    return cw;
+  };
+  int si = __builtin_amdgcn_readfirstlane(slice_at(A, A.rev ? lo + end - 1 - s : s));
+  int W = cs[si].width;
+  int o[8];
+  {
+    const int pb = cs[si].dict;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = pat[pb + min(j, W - 1)];
+  }
+  Ull2 cw = code_at(cs[si].ioff);
+  for (;;) {
+    const int ns = s + step;
+    const bool has_next = ns < end;
+    const int nk = has_next ? ns : s;
+    const int sn = __builtin_amdgcn_readfirstlane(slice_at(A, A.rev ? lo + end - 1 - nk : nk));
+    const int Wn = cs[sn].width, pbn = cs[sn].dict;
+    const int64_t coffn = cs[sn].ioff;
+    const int r0 = si * (2 * kSellRows) + 2 * lane;
+    const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
+    const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
+    epi.pre2(rc0, rc1);
+    T g0[8], g1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int base = r0 + o[j];
+      const int cb = min(max(base, 0), nxm2);
+      if constexpr ((V & 16) != 0) {
+        g0[j] = T(cb & 1);
+        g1[j] = T(cb & 2);
+      } else {
+        const auto g = x.pair(cb);
+        g0[j] = base <= nxm2 ? g.x : g.y;
+        g1[j] = base >= 0 ? g.y : g.x;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int on[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) on[j] = pat[pbn + min(j, Wn - 1)];
+    const Ull2 cwn = code_at(coffn);
+    __builtin_amdgcn_sched_barrier(0);
+    T acc0 = T(0), acc1 = T(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      unsigned k0, k1;
+      bool on0, on1;
+      if constexpr (C4) {
+        k0 = (unsigned)(cw.x >> (8 * j)) & 0xfu;
+        k1 = (unsigned)(cw.x >> (8 * j + 4)) & 0xfu;
+        on0 = k0 != 0xfu;
+        on1 = k1 != 0xfu;
+      } else {
+        const unsigned long long w = j < 4 ? cw.x : cw.y;
+        k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
+        k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
+        on0 = k0 != kVcAbsent;
+        on1 = k1 != kVcAbsent;
+      }
+      const T t0 = acc0 + vd[k0] * g0[j];
+      const T t1 = acc1 + vd[k1] * g1[j];
+      acc0 = on0 ? t0 : acc0;
+      acc1 = on1 ? t1 : acc1;
+    }
+    epi.row2(r0, acc0, acc1, l0, l1);
+    if (!has_next) break;
+    si = sn;
+    W = Wn;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = on[j];
+    cw = cwn;
+    s = ns;
+  }
 }
 
 template <typename T, int V, class Epi, class Gather>
@@ -1288,6 +1412,10 @@ __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, E
   const T *__restrict__ src = static_cast<const T *>(A.svdict);
   for (int i = threadIdx.x; i < kVcDict; i += kBlock) vd[i] = src[i];
   __syncthreads();
+  if constexpr ((V & 524288) != 0) {
+    spmv_sellpv_pipe<T, V, Epi, Gather>(A, x, epi, vd);
+    return;
+  }
   int s, step, end, lo;
   sell_range((int)A.nsl, s, step, end, lo);
   for (; s < end; s += step)
@@ -1930,6 +2058,23 @@ __global__ __launch_bounds__(kBlock) void k_sellpv_pack(int64_t n, int64_t nsl,
   }
 }
 
+// 4-bit value codes from the 8-bit ones (dictionary of at most kVc4Max
+// values): chunk-lane t's 16 bytes (slot j: bytes 2 j, 2 j + 1 for rows 0, 1)
+// become 8 bytes, byte j = row 0's code | row 1's code << 4, kVcAbsent -> 0xf.
+__global__ __launch_bounds__(kBlock) void k_vc_narrow(const unsigned char *__restrict__ c8,
+                                                      unsigned char *__restrict__ c4,
+                                                      int64_t chunks) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < chunks; t += stride) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned a = c8[t * 16 + 2 * j], b = c8[t * 16 + 2 * j + 1];
+      c4[t * 8 + j] = (unsigned char)((a == kVcAbsent ? 0xfu : a) |
+                                      ((b == kVcAbsent ? 0xfu : b) << 4));
+    }
+  }
+}
+
 // Poisson rows [row_begin, row_end): columns ascending (-z,-y,-x,d,+x,+y,+z).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_poisson(int dim, int nx, int ny, int nz,
@@ -1971,7 +2116,7 @@ inline int elem_grid(int64_t n, int per_thread) {
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
                  A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
-                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict};
+                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4};
 }
 
 }  // namespace
@@ -2189,7 +2334,9 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     // the variant follows the SELL copy's layout: bit 4096 for 2 rows per
     // lane; pipelined (bit 8) for 1 row per lane and slices <= 8 wide
     if (A.sl && A.sell_kind && (v & 32768) && A.svc)
-      return 32768 | 8192 | (v & (16 | 2 | 65536 | 131072));
+      return 32768 | 8192 |
+             (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
+                   (A.sell_maxw <= 8 ? 524288 : 0)));
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2269,6 +2416,12 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 24578: CGX_LAUNCH_V(KERNEL, 24578, __VA_ARGS__);                             \
     case 40960: CGX_LAUNCH_V(KERNEL, 40960, __VA_ARGS__);                             \
     case 40962: CGX_LAUNCH_V(KERNEL, 40962, __VA_ARGS__);                             \
+    case 303104: CGX_LAUNCH_V(KERNEL, 303104, __VA_ARGS__);                           \
+    case 303106: CGX_LAUNCH_V(KERNEL, 303106, __VA_ARGS__);                           \
+    case 565248: CGX_LAUNCH_V(KERNEL, 565248, __VA_ARGS__);                           \
+    case 565250: CGX_LAUNCH_V(KERNEL, 565250, __VA_ARGS__);                           \
+    case 827392: CGX_LAUNCH_V(KERNEL, 827392, __VA_ARGS__);                           \
+    case 827394: CGX_LAUNCH_V(KERNEL, 827394, __VA_ARGS__);                           \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -2283,7 +2436,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(67) X(68) X(69) X(70) X(71) X(524) X(525) X(526) X(527) X(264) X(265) X(266)      \
   X(267) X(140) X(141) X(142) X(143) X(76) X(77) X(78) X(79) X(2048) X(2050) X(2056)  \
   X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)        \
-  X(40978) X(106498) X(172034)
+  X(40978) X(106498) X(172034) X(303104) X(303106) X(303122) X(827392) X(827394)        \
+  X(827410) X(565248) X(565250)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \
@@ -2384,6 +2538,8 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 40978: CGX_LAUNCH_V(k_spmv_dot, 40978, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 106498: CGX_LAUNCH_V(k_spmv_dot, 106498, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 172034: CGX_LAUNCH_V(k_spmv_dot, 172034, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 303122: CGX_LAUNCH_V(k_spmv_dot, 303122, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 827410: CGX_LAUNCH_V(k_spmv_dot, 827410, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -2524,6 +2680,14 @@ hipError_t Launch<T>::sellpv_pack(const CsrDev &A, const T *val, const T *dict, 
   const int g = elem_grid(A.nsl * kSellRows * 2, 4);
   hipLaunchKernelGGL(k_sellpv_pack<T>, dim3(g), dim3(kBlock), 0, s, A.n, A.nsl, A.rowptr, A.col,
                      val, A.sl, A.sdict, dict, nd, codes, miss, missv);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t Launch<T>::vc_narrow(const void *codes8, void *codes4, int64_t chunks,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(k_vc_narrow, dim3(elem_grid(chunks, 4)), dim3(kBlock), 0, s,
+                     (const unsigned char *)codes8, (unsigned char *)codes4, chunks);
   return hipGetLastError();
 }
 

@@ -19,7 +19,8 @@ from tests.util import rel
 
 pytestmark = pytest.mark.gpu
 
-VC = [34816, 34818]          # SELL-P with value codes: default / non-temporal loads
+VC = [34816, 34818, 559104, 559106]  # value codes: default / non-temporal loads; pipelined
+VC4 = [296960, 296962, 821248, 821250]  # 4-bit codes (at most 15 distinct values)
 PLAIN = [8192, 8194, 13]     # SELL-P values, CSR-stream
 
 
@@ -84,13 +85,20 @@ def test_value_codes_bitexact(queue, oracle, case, dtype):
     if EXPECT_CODES[case] is not None:
         assert nv == EXPECT_CODES[case]
     x = np.random.default_rng(3).standard_normal(n)
-    out = spmv_all(queue, A, x, VC + PLAIN, dtype)
+    vc4 = VC4 if nv <= 15 else []
+    if not vc4:
+        with pytest.raises(CgxError, match="4-bit"):
+            check(lib().cgx_csr_set_variant(A.schedule(), VC4[0]))
+    out = spmv_all(queue, A, x, VC + vc4 + PLAIN, dtype)
     v = C.c_int()
-    check(lib().cgx_csr_set_variant(A.schedule(), 34818))
-    check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
-    assert v.value == 40962
+    for set_v, want in ((34818, 40962), (296962, 303106)):
+        if set_v in VC4 and not vc4:
+            continue
+        check(lib().cgx_csr_set_variant(A.schedule(), set_v))
+        check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
+        assert v.value == want, (set_v, v.value)
     ref = oracle.spmv(rp, cl, vl, x) if dtype == np.float64 else out[8192]
-    for k in VC + PLAIN:
+    for k in VC + vc4 + PLAIN:
         np.testing.assert_array_equal(out[k], ref, err_msg=f"variant {k}")
 
 
@@ -131,9 +139,9 @@ def test_value_codes_signed_zero_and_nonfinite(queue, oracle):
     A = Matrix(queue, vl, cl, rp)
     check(lib().cgx_csr_set_sell(A.schedule(), 3))
     assert n_codes(A) == 5
-    y = spmv_all(queue, A, x, VC)
+    y = spmv_all(queue, A, x, VC + VC4)
     ref = oracle.spmv(rp, cl, vl, x)
-    for k in VC:
+    for k in VC + VC4:
         np.testing.assert_array_equal(np.isnan(y[k]), np.isnan(ref))
         ok = ~np.isnan(ref)
         np.testing.assert_array_equal(y[k][ok], ref[ok])
