@@ -162,7 +162,7 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
   T *Ap = (T *)cg->Ap;
   int rc;
   const bool halo = A->dist && A->halo.n_ghost + A->halo.send_total > 0;
-  if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & 2048)) {
+  if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192))) {
     bool async = false;
     if ((rc = dist_halo_post(A, p, s, &async))) return rc;
     const int gi = Launch<T>::slice_grid(A->dev, A->split_ni);
@@ -718,6 +718,8 @@ void free_sell(cgx_csr *A) {
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
   A->sell_padded = 0;
+  A->sell_idx_words = 0;
+  A->vc_chunks = 0;
 }
 
 // SELL layout of a host CSR (cgx_internal.h SellSlice; DESIGN.md §SpMV
@@ -1034,6 +1036,7 @@ template <typename T> static int build_value_codes_t(cgx_csr *A) {
   A->dev.svc = codes;
   A->dev.svdict = ddict;
   A->dev.nvdict = (int)dict.size();
+  A->vc_chunks = chunks;
   if ((int)dict.size() <= kVc4Max) {  // 4-bit codes: half the code stream
     void *c4 = nullptr;
     e = hipMalloc(&c4, (size_t)chunks * 8);
@@ -1163,6 +1166,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   A->dev.sell_maxw = 0;
   for (const SellSlice &m : sl) A->dev.sell_maxw = std::max(A->dev.sell_maxw, m.width);
   A->sell_padded = voff;
+  A->sell_idx_words = (int64_t)idx.size();
   if (kind && A->dtype == CGX_F32)
     e = Launch<float>::sellp_pack(A->dev, (const float *)A->dev.val, (float *)A->d_sell_val,
                                   A->d_sell_mask, s);
@@ -1199,6 +1203,22 @@ extern "C" int cgx_csr_set_sell(cgx_csr *A, int rows_per_lane) {
   int rc = build_sell(A, nullptr, nullptr, rows_per_lane);
   if (rc) return rc;
   if (!A->dev.sl && (A->dev.variant & (2048 | 8192))) A->dev.variant = 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
+  CGX_REQUIRE(A && bytes, CGX_EINVAL, "NULL argument");
+  const int v = launch_variant(A->dev, A->dtype);
+  const int64_t es = (int64_t)dtype_size(A->dtype), nsl = A->dev.nsl;
+  const int64_t desc = nsl * (int64_t)sizeof(SellSlice);
+  if (v & 32768)
+    *bytes = ((v & 262144) ? 8 : 16) * A->vc_chunks + desc;
+  else if (v & 8192)
+    *bytes = es * A->sell_padded + nsl * 2 * kSellRows * ((v & 16384) ? 4 : 1) + desc;
+  else if (v & 2048)
+    *bytes = es * A->sell_padded + 8 * A->sell_idx_words + desc;
+  else
+    *bytes = (es + 4) * A->dev.nnz + 4 * (A->dev.n + 1);
   return CGX_OK;
 }
 

@@ -100,6 +100,8 @@ struct cgx_csr {
   int split_ni = 0, split_nb = 0;
   hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
   int64_t sell_padded = 0;
+  int64_t sell_idx_words = 0;  // dictionary SELL index words
+  int64_t vc_chunks = 0;       // value-code chunk-lanes (16 B each, 8 B in 4-bit form)
 };
 
 struct cgx_cg {

@@ -99,6 +99,11 @@ int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
  * cgx_csr_create when the SELL-P copy exists and the matrix has that few
  * distinct values; $CGX_VALUE_CODES=0 disables it), 0 when it has none. */
 int cgx_csr_value_codes(cgx_csr *csr, int *n_values);
+/* Bytes of the matrix stream one SpMV launch in the matrix's current
+ * variant reads (values, indices / codes / masks, slice descriptors;
+ * vectors excluded): the format's algorithmic bytes, next to CSR's
+ * 12 nnz + 4 (n + 1) in fp64. */
+int cgx_csr_stream_bytes(cgx_csr *csr, int64_t *bytes);
 
 /* ---- VectorOperations<DT> (src/VectorOperations.hpp) ----------------------
  * Scalars are DEVICE pointers, as in the reference (Scalar<DT>::ptr()). */

@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
-variant = int(sys.argv[2]) if len(sys.argv) > 2 else 8194
+variant = int(sys.argv[2]) if len(sys.argv) > 2 else 827394
 kern = f"k_spmv_dot<double, {variant}>"
 
 
@@ -42,7 +42,12 @@ out = {
                "MI355X_MICROARCH.md HBM/rocprofv3 section); KB = 1024 B"),
     "raw": f"profiles/{tag}_pmc_spmv.txt",
     "algorithmic_bytes_per_launch": 12 * nnz + 4 * (n + 1) + 16 * n,
-    "note": ("SELL-P copy: 8 B value per slot (+1.3% padding) and a 1-byte slot mask per row "
+    "note": ("SELL-P copy with value codes: per row pair and chunk of 8 slots one 8-byte "
+             "word of 4-bit codes into the matrix's value dictionary (2 values at 256^3), "
+             "offset patterns per 128-row slice; instead of CSR's 12 B per entry + 4 B rowptr "
+             "per row, so traffic is far below the CSR-format algorithmic bytes"
+             if variant & 32768 else
+             "SELL-P copy: 8 B value per slot (+1.3% padding) and a 1-byte slot mask per row "
              "instead of CSR's 12 B per entry + 4 B rowptr per row, so traffic is below the "
              "CSR-format algorithmic bytes"),
 }
