@@ -1240,7 +1240,7 @@ static bool known_variant(int v) {
                            68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
                            34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
-                           821248, 821250};
+                           821248, 821250, 1607680, 1607682, 1869824, 1869826};
   for (int k : ok)
     if (k == v) return true;
   return false;
@@ -1292,10 +1292,12 @@ int autotune_spmv(cgx_csr *A) {
     cands.push_back(2050);
   }
   // SELL-P value codes: 1 B per slot instead of 8 (4-bit codes: 0.5 B), and
-  // their software-pipelined loop (bit 524288) where no slice is over 8 wide
+  // their software-pipelined loop (bit 524288) where no slice is over 8 wide,
+  // that loop with the +-1 neighbours taken from the adjacent lanes (bit
+  // 1048576: one gather pair fewer per offset -1 / +1)
   for (int c4 : {0, 262144}) {
     if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
-    for (int pipe : {0, 524288}) {
+    for (int pipe : {0, 524288, 524288 | 1048576}) {
       if (pipe && A->dev.sell_maxw > 8) continue;
       if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
       cands.push_back(2050 | 32768 | c4 | pipe);

@@ -321,6 +321,16 @@ template <typename T> struct GatherX {
   __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
     return *reinterpret_cast<const typename PairU<T>::V *>(x + c);
   }
+  // the pair at byte offset b (< 4 GiB): a scalar base plus a 32-bit vector
+  // offset, one VALU add per gather instead of a 64-bit address
+  __device__ __forceinline__ typename PairU<T>::V pair_b(unsigned b) const {
+    return *reinterpret_cast<const typename PairU<T>::V *>(reinterpret_cast<const char *>(x) +
+                                                           b);
+  }
+  // element i by a scalar load (uniform i)
+  __device__ __forceinline__ T at_s(int i) const {
+    return ((const __attribute__((address_space(4))) T *)x)[i];
+  }
 };
 template <typename T> struct GatherP {
   const T *__restrict__ r;
@@ -334,6 +344,19 @@ template <typename T> struct GatherP {
     o.x = a.x + beta * b.x;
     o.y = a.y + beta * b.y;
     return o;
+  }
+  __device__ __forceinline__ typename PairU<T>::V pair_b(unsigned b) const {
+    using U = typename PairU<T>::V;
+    const U a = *reinterpret_cast<const U *>(reinterpret_cast<const char *>(r) + b);
+    const U q = *reinterpret_cast<const U *>(reinterpret_cast<const char *>(pp) + b);
+    U o;
+    o.x = a.x + beta * q.x;
+    o.y = a.y + beta * q.y;
+    return o;
+  }
+  __device__ __forceinline__ T at_s(int i) const {
+    return ((const __attribute__((address_space(4))) T *)r)[i] +
+           beta * ((const __attribute__((address_space(4))) T *)pp)[i];
   }
 };
 
@@ -1303,6 +1326,34 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
   epi.row2(r0, acc0, acc1, l0, l1);
 }
 
+// Whole-wave lane shifts by one (DPP wave_shr:1 / wave_shl:1): lane l gets
+// lane l - 1's (l + 1's) value; lane 0 (63), which has no source, keeps
+// `edge`.
+template <typename T> __device__ __forceinline__ T wave_shr1(T v, T edge);
+template <typename T> __device__ __forceinline__ T wave_shl1(T v, T edge);
+template <> __device__ __forceinline__ double wave_shr1(double v, double edge) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), 0x138, 0xf,
+                                             0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x138, 0xf,
+                                             0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <> __device__ __forceinline__ double wave_shl1(double v, double edge) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), 0x130, 0xf,
+                                             0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x130, 0xf,
+                                             0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <> __device__ __forceinline__ float wave_shr1(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v),
+                                                    0x138, 0xf, 0xf, false));
+}
+template <> __device__ __forceinline__ float wave_shl1(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v),
+                                                    0x130, 0xf, 0xf, false));
+}
+
 // Software-pipelined value-code SELL-P (variant bit 524288; every slice at
 // most 8 wide, i.e. one code chunk): while slice s gathers and sums, the
 // next slice's descriptor and offset pattern (a dependent pair of scalar
@@ -1313,6 +1364,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
                                                  const T *__restrict__ vd) {
   constexpr bool NT = (V & 2) != 0;
   constexpr bool C4 = (V & 262144) != 0;
+  constexpr bool CR = (V & 1048576) != 0;  // stencil slices: +-1 by lane shifts
   const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
   const auto *pat = (const __attribute__((address_space(4))) int *)A.sdict;
   const Ull2 *__restrict__ codes = static_cast<const Ull2 *>(A.svc);
@@ -1342,6 +1394,15 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     for (int j = 0; j < 8; ++j) o[j] = pat[pb + min(j, W - 1)];
   }
   Ull2 cw = code_at(cs[si].ioff);
+  // slice si is interior when the pairs of its lowest and highest offset
+  // (o[0], o[7] = o[W-1]: the pattern is sorted) lie inside x for every
+  // lane, dead lanes of a last partial slice included, and byte offsets
+  // into x fit 32 bits
+  const bool off32 = (uint64_t)A.nx * sizeof(T) < (uint64_t(1) << 32);
+  auto inner_slice = [&](int sl, int omin, int omax) {
+    const int fr = sl * (2 * kSellRows);
+    return off32 && fr + omin >= 0 && fr + 2 * kSellRows - 2 + omax <= nxm2;
+  };
   for (;;) {
     const int ns = s + step;
     const bool has_next = ns < end;
@@ -1352,19 +1413,75 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     const int r0 = si * (2 * kSellRows) + 2 * lane;
     const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
     const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
-    epi.pre2(rc0, rc1);
     T g0[8], g1[8];
+    const bool inner = inner_slice(si, o[0], o[7]);
+    // stencil slices (bit 1048576): offsets -1, 0, +1 in slots K..K+2 of a
+    // WW-wide pattern (K = 2, WW = 7: the 3-D 7-point interior; K = 1,
+    // WW = 5: 2-D 5-point). The center pair x[r0], x[r0 + 1] is one aligned
+    // load (and the dot's p); x[r0 - 1] and x[r0 + 2] come from the
+    // neighbour lanes (DPP wave shifts), the slice's outer two, x[first - 1]
+    // and x[first + 128], from scalar loads: three vector loads fewer per
+    // slice. Every vector load is issued before the shifts wait.
+    auto near = [&](auto kc, auto wc) {
+      constexpr int K = decltype(kc)::value, WW = decltype(wc)::value;
+      const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
+      const auto c = x.pair_b(rb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int base = r0 + o[j];
-      const int cb = min(max(base, 0), nxm2);
-      if constexpr ((V & 16) != 0) {
-        g0[j] = T(cb & 1);
-        g1[j] = T(cb & 2);
-      } else {
-        const auto g = x.pair(cb);
-        g0[j] = base <= nxm2 ? g.x : g.y;
-        g1[j] = base >= 0 ? g.y : g.x;
+      for (int j = 0; j < 8; ++j) {
+        if (j < K || (j > K + 2 && j < WW)) {
+          const auto g = x.pair_b(rb + (unsigned)(o[j] * (int)sizeof(T)));
+          g0[j] = g.x;
+          g1[j] = g.y;
+        } else if (j >= WW) {
+          g0[j] = g1[j] = T(0);
+        }
+      }
+      const int fr = si * (2 * kSellRows);
+      const T elo = x.at_s(fr - 1), ehi = x.at_s(fr + 2 * kSellRows);
+      __builtin_amdgcn_sched_barrier(0);
+      const T left = wave_shr1(c.y, elo), right = wave_shl1(c.x, ehi);
+      g0[K] = left;
+      g1[K] = c.x;
+      g0[K + 1] = c.x;
+      g1[K + 1] = c.y;
+      g0[K + 2] = c.y;
+      g1[K + 2] = right;
+      epi.pre2c(rc0, rc1, c.x, c.y);
+    };
+    if (CR && inner && W == 7 && o[2] == -1 && o[3] == 0 && o[4] == 1) {
+      near(std::integral_constant<int, 2>{}, std::integral_constant<int, 7>{});
+    } else if (CR && inner && W == 5 && o[1] == -1 && o[2] == 0 && o[3] == 1) {
+      near(std::integral_constant<int, 1>{}, std::integral_constant<int, 5>{});
+    } else if (inner) {
+      // interior slice (uniform): every pair lies inside x, so no clamps and
+      // no end selects; the address is one 32-bit add to a scalar base
+      epi.pre2(rc0, rc1);
+      const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr ((V & 16) != 0) {
+          g0[j] = T(rb & 1);
+          g1[j] = T(rb & 2);
+        } else {
+          const auto g = x.pair_b(rb + (unsigned)(o[j] * (int)sizeof(T)));
+          g0[j] = g.x;
+          g1[j] = g.y;
+        }
+      }
+    } else {
+      epi.pre2(rc0, rc1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int base = r0 + o[j];
+        const int cb = min(max(base, 0), nxm2);
+        if constexpr ((V & 16) != 0) {
+          g0[j] = T(cb & 1);
+          g1[j] = T(cb & 2);
+        } else {
+          const auto g = x.pair(cb);
+          g0[j] = base <= nxm2 ? g.x : g.y;
+          g1[j] = base >= 0 ? g.y : g.x;
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1450,9 +1567,14 @@ __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__
 // waits on the prefetch); row(i, s) consumes the row sum.
 // pre2 / row2: the same for two rows (SELL with 2 rows per lane); a row
 // past the matrix end is given clamped (pre2) and flagged dead (row2).
+// pre2c(i0, i1, c0, c1): pre2 when the gathered vector's elements at the
+// two rows, c0 = x[i0], c1 = x[i1], are already in registers (the
+// value-code kernel's center pair); only EpiDot, whose p IS the gathered
+// vector (k_spmv_dot), uses them.
 template <typename T> struct EpiStore {
   T *__restrict__ y;
   __device__ __forceinline__ void pre(int) {}
+  __device__ __forceinline__ void pre2c(int, int, T, T) {}
   __device__ __forceinline__ void row(int i, T s) { y[i] = s; }
   __device__ __forceinline__ void pre2(int, int) {}
   __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
@@ -1465,6 +1587,10 @@ template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
   const T *__restrict__ p;
   T acc, pv, pv1;
   __device__ __forceinline__ void pre(int i) { pv = p[i]; }
+  __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
+    pv = c0;
+    pv1 = c1;
+  }
   __device__ __forceinline__ void row(int i, T s) {
     Ap[i] = s;
     acc += s * pv;
@@ -1501,6 +1627,7 @@ template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
   T *__restrict__ p;
   T acc, bv, bv1;
   __device__ __forceinline__ void pre(int i) { bv = b[i]; }
+  __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
   __device__ __forceinline__ void row(int i, T s) {
     const T ri = bv - s;
     r[i] = ri;
@@ -1533,6 +1660,7 @@ template <typename T> struct EpiFused {
   T alpha, beta;
   bool do_x;
   T acc, rv, pv, xv, rv1, pv1, xv1;
+  __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
   __device__ __forceinline__ void pre(int i) {
     rv = r[i];
     pv = pp[i];
@@ -1566,6 +1694,7 @@ template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
   T acc0, acc1, bv, xv, bv1, xv1;
+  __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
   __device__ __forceinline__ void pre(int i) {
     bv = b[i];
     xv = x[i];
@@ -2336,7 +2465,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     if (A.sl && A.sell_kind && (v & 32768) && A.svc)
       return 32768 | 8192 |
              (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
-                   (A.sell_maxw <= 8 ? 524288 : 0)));
+                   (A.sell_maxw <= 8 ? 524288 | 1048576 : 0)));
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2422,6 +2551,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 565250: CGX_LAUNCH_V(KERNEL, 565250, __VA_ARGS__);                           \
     case 827392: CGX_LAUNCH_V(KERNEL, 827392, __VA_ARGS__);                           \
     case 827394: CGX_LAUNCH_V(KERNEL, 827394, __VA_ARGS__);                           \
+    case 1613824: CGX_LAUNCH_V(KERNEL, 1613824, __VA_ARGS__);                         \
+    case 1613826: CGX_LAUNCH_V(KERNEL, 1613826, __VA_ARGS__);                         \
+    case 1875968: CGX_LAUNCH_V(KERNEL, 1875968, __VA_ARGS__);                         \
+    case 1875970: CGX_LAUNCH_V(KERNEL, 1875970, __VA_ARGS__);                         \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -2437,7 +2570,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(267) X(140) X(141) X(142) X(143) X(76) X(77) X(78) X(79) X(2048) X(2050) X(2056)  \
   X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)        \
   X(40978) X(106498) X(172034) X(303104) X(303106) X(303122) X(827392) X(827394)        \
-  X(827410) X(565248) X(565250)
+  X(827410) X(565248) X(565250) X(1613824) X(1613826) X(1875968) X(1875970)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \

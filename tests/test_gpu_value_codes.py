@@ -19,8 +19,10 @@ from tests.util import rel
 
 pytestmark = pytest.mark.gpu
 
-VC = [34816, 34818, 559104, 559106]  # value codes: default / non-temporal loads; pipelined
-VC4 = [296960, 296962, 821248, 821250]  # 4-bit codes (at most 15 distinct values)
+# value codes: default / non-temporal loads; pipelined; pipelined with the
+# +-1 neighbours from the adjacent lanes (bit 1048576)
+VC = [34816, 34818, 559104, 559106, 1607680, 1607682]
+VC4 = [296960, 296962, 821248, 821250, 1869824, 1869826]  # 4-bit codes (<= 15 values)
 PLAIN = [8192, 8194, 13]     # SELL-P values, CSR-stream
 
 
@@ -171,3 +173,24 @@ def test_cg_with_value_codes_matches_plain(oracle, monkeypatch, dim, n):
     xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-8)
     assert abs(xs["1"][1] - res.iterations) <= 2
     assert rel(xs["1"][0], xr) <= 1e-10
+
+
+@pytest.mark.parametrize("dim,n", [(2, 100), (3, 27)])
+def test_cg_every_value_code_form_in_the_loop(oracle, monkeypatch, dim, n):
+    """Every value-code form forced into the CG loop (k_cg_init and the
+    fused k_spmv_dot, whose p.Ap takes the center pair from the gather in the
+    lane-shift form) gives the plain SELL-P run's x and iteration count bit
+    for bit; ragged sizes leave partial last slices."""
+    rp, cl, vl = oracle.poisson(dim, n, n + 1, n - 2 if dim == 3 else 1)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    out = {}
+    for v in [8194] + VC + VC4:
+        monkeypatch.setenv("CGX_SPMV_VARIANT", str(v))
+        cg = cga.CG.createCG()
+        cg.setMatrix(vl, cl, rp)
+        cg.setTarget(b)
+        cg.solve(1e-10)
+        out[v] = (cg.extract(), cg.iterations)
+    for v in VC + VC4:
+        np.testing.assert_array_equal(out[v][0], out[8194][0], err_msg=f"variant {v}")
+        assert out[v][1] == out[8194][1], v
