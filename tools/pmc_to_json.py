@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
-variant = int(sys.argv[2]) if len(sys.argv) > 2 else 827394
+variant = int(sys.argv[2]) if len(sys.argv) > 2 else 1875970
 kern = f"k_spmv_dot<double, {variant}>"
 
 
