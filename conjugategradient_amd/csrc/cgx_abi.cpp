@@ -1275,7 +1275,7 @@ int autotune_spmv(cgx_csr *A) {
   if (bytes < (int64_t(64) << 20)) {  // small: the size heuristic, SELL where built
     if (A->dev.sl)
       A->dev.variant = (A->dev.svc4 ? (2048 | 32768 | 262144) : A->dev.svc ? (2048 | 32768) : 2048) |
-                       (A->dev.svc && A->dev.sell_maxw <= 8 ? 524288 : 0);
+                       (A->dev.svc && A->dev.sell_maxw <= 8 ? 524288 | 1048576 : 0);
     return CGX_OK;
   }
   // (the software-pipelined SELL forms, 2056/2058, measured slower than the
