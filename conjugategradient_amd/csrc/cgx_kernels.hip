@@ -301,6 +301,41 @@ __device__ __forceinline__ Int2 tail_cols(Int2 c, int e0, int kk1) {
   return c;
 }
 
+// Non-temporal loads and stores for the vector streams whose data is not
+// read again before far more than the 256 MB Infinity Cache has streamed
+// past (Ap after k_update_r, x and the old p buffers in the flushing body):
+// they then leave the cache to the vectors that the next kernel re-reads
+// ("cache policy").
+#ifdef CGX_NO_STREAM_NT
+constexpr bool kStreamNt = false;
+#else
+constexpr bool kStreamNt = true;
+#endif
+// HIP vector types (double2, float2 of element T): non-temporal through the
+// native vector of two T
+template <bool NT, typename T, typename P> __device__ __forceinline__ P ldv(const P *p) {
+  if constexpr (NT) {
+    typedef T N __attribute__((ext_vector_type(2)));
+    const N v = __builtin_nontemporal_load(reinterpret_cast<const N *>(p));
+    P r;
+    r.x = v.x;
+    r.y = v.y;
+    return r;
+  } else {
+    return *p;
+  }
+}
+template <bool NT, typename T, typename P> __device__ __forceinline__ void stv(P *p, P v) {
+  if constexpr (NT) {
+    typedef T N __attribute__((ext_vector_type(2)));
+    N n;
+    n.x = v.x;
+    n.y = v.y;
+    __builtin_nontemporal_store(n, reinterpret_cast<N *>(p));
+  } else {
+    *p = v;
+  }
+}
 template <bool NT, typename P> __device__ __forceinline__ P ldg(const P *p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
@@ -1888,7 +1923,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
   for (int u = 0; u < 4; ++u) {  // clamped (r and Ap have a slack element): no branch
     const int64_t j = E(min(i + u * stride, n2 > 0 ? n2 - 1 : 0));
     rv[u] = ri2[j];
-    av[u] = a2[j];
+    av[u] = ldv<kStreamNt, T>(a2 + j);  // Ap is dead after this kernel
   }
   const T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
   const T alpha = rxr / pAp;
@@ -1903,7 +1938,7 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         rv[u] = ri2[E(i + u * stride)];
-        av[u] = a2[E(i + u * stride)];
+        av[u] = ldv<kStreamNt, T>(a2 + E(i + u * stride));
       }
     }
 #pragma unroll
@@ -2337,10 +2372,10 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
     const V pv = p2[i];
     const V rv = rv2[i];
     V q[3], xv;
-    if constexpr (FLUSH) {
-      xv = x2[i];
+    if constexpr (FLUSH) {  // x and the old p buffers: not read again soon
+      xv = ldv<kStreamNt, T>(x2 + i);
 #pragma unroll
-      for (int t = 0; t < 3; ++t) q[t] = Q[t][i];  // before pn (= P0) is written
+      for (int t = 0; t < 3; ++t) q[t] = ldv<kStreamNt, T>(Q[t] + i);  // before pn (= P0) is written
     }
     V o;
     o.x = rv.x + beta * pv.x;
@@ -2357,7 +2392,7 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
         xv.x = xv.x + a[3] * pv.x;
         xv.y = xv.y + a[3] * pv.y;
       }
-      x2[i] = xv;
+      stv<kStreamNt, T>(x2 + i, xv);
     }
     pn2[i] = o;
   };
