@@ -2314,8 +2314,14 @@ template <typename T> int Launch<T>::grid_rows(int nrb) {
 // 8-per-CU persistent grid the SpMV uses: k_update_r 256 (1 per CU), the
 // x/p updates 512 (2 per CU; the flushing body keeps 8 streams in flight);
 // A/B in DESIGN.md §4 (gpurun_out r44/r45).
-constexpr int kGridUpdateR = 256;
-constexpr int kGridUpdateP = 512;
+#ifndef CGX_GRID_UPDATE_R
+#define CGX_GRID_UPDATE_R 256
+#endif
+#ifndef CGX_GRID_UPDATE_P
+#define CGX_GRID_UPDATE_P 512
+#endif
+constexpr int kGridUpdateR = CGX_GRID_UPDATE_R;  // A/B builds: EXTRA=-DCGX_GRID_UPDATE_R=...
+constexpr int kGridUpdateP = CGX_GRID_UPDATE_P;
 template <typename T> int Launch<T>::grid_elems(int64_t n, int cap) {
   int64_t g = (n + (int64_t)kBlock * 8 - 1) / ((int64_t)kBlock * 8);
   if (g < 1) g = 1;
