@@ -1,102 +1,200 @@
 #!/usr/bin/env python3
 """Benchmark of the CG hot path (BASELINE.json metric) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256] [--weak]
 
 A "step" is one CG iteration (loop body of CG::solve, src/CG.hpp:359-436):
 SpMV + p.Ap, r-update + r.r, x/p-update, on synthetic 3-D 7-point Dirichlet
 Poisson CSR (fp64 values, int32 indices, b_i = i + 1, x0 = 0).
 
 * N = 1: the 256^3 grid (the metric's headline config) on one GPU.
-* N > 1 (launched with torch.distributed.run, one rank per GPU): weak
-  scaling — every rank owns a 256^3 z-slab of a 256 x 256 x (256 N) grid;
-  halo exchange of p and the two dot all-reduces go over RCCL.
+* N > 1: strong scaling by default — the same global grid (256^3; --grid 512
+  is BASELINE config 4) split into contiguous z-slabs, one rank per GPU;
+  the halo exchange of p and the two dot all-reduces run over xGMI (device
+  peer transport where it passes its self-test, else RCCL). --weak gives
+  every rank its own 256^3 slab instead.
+* `python bench.py --gpus N` with no launcher environment starts its own N
+  ranks (torch.distributed.run, 127.0.0.1) as a child process before touching
+  any GPU; under a launcher, WORLD_SIZE must equal --gpus.
 
-value = algorithmic HBM bytes of one iteration over the whole job
-(B_alg = 12 nnz + 4 (N+1) + 80 N) x iterations/s, in GB/s.
-Inputs are generated directly in HBM before the timed region.
+value = the COMPULSORY HBM bytes of one iteration in the formats the kernels
+stream (the SpMV's matrix stream from cgx_csr_stream_bytes, p read and Ap
+written, 24 N for the r update, 34 N average for the deferred x/p update),
+summed over ranks, x iterations/s, in GB/s — a physical figure (<= peak).
+The CSR-priced figure of SURVEY §8(d) (B_alg = 12 nnz + 4 (N+1) + 80 N) is
+reported beside it as `csr_equivalent_GBs`.
 
-The timed region replays hipGraphs of the iteration (no per-kernel events:
-recording events between kernels costs ~10 us per kernel). Right after it,
-the same solver runs `--profile-steps` more iterations with HIP events around
-every kernel on the solver stream; rank 0 reports the dominant kernel's
-roofline (k_spmv_dot) from those. At N = 1 rank 0 also times a CPU baseline:
-the oracle's OpenMP restatement of the reference's iteration
-(oracle/cg_oracle.c) on a bounded sample of the same workload.
+The timed region replays hipGraphs of the iteration (no per-kernel events).
+Right after it, `--profile-steps` more iterations run with HIP events around
+every kernel on the solver stream (the stream the kernels run on); rank 0
+reports the dominant kernel's roofline (k_spmv_dot) from those, priced at
+its own format's compulsory bytes. At N = 1 rank 0 also reports:
+  * `csr_general`: the same 256^3 matrix solved with the general-value
+    formats (plain SELL-P values, and CSR-stream — the path of a matrix with
+    many distinct values such as G3_circuit);
+  * `cpu_baseline`: the oracle's OpenMP restatement of the reference
+    iteration (oracle/cg_oracle.c) on every core this job may use, on a
+    bounded sample of the same workload.
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402  (before libcgx: one HIP runtime per process)
-import torch.distributed as dist  # noqa: E402
-
-import conjugategradient_amd as cga  # noqa: E402
-from conjugategradient_amd._native import F64, check, lib  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+METRIC = "CG iterations/sec + achieved HBM GB/s, 256³ 7-pt Poisson fp64, 1/2/4/8 GPUs"
 
 
 def b_alg(n: int, nnz: int) -> int:
-    """Algorithmic bytes of one fused CG iteration."""
+    """CSR-priced bytes of one fused CG iteration."""
     return 12 * nnz + 4 * (n + 1) + 80 * n
 
 
-def spmv_dot_bytes(n: int, nnz: int, fused: bool) -> int:
-    """Algorithmic bytes of one launch of the dominant kernel.
-    k_spmv_dot (3-kernel mode): val 8 + col 4 per entry, rowptr 4 per row,
-    p read 8 and Ap written 8 per row.
-    k_spmv_fused (fused mode): the same CSR stream, plus per row r, p_old, x
-    read (24) and p_new, x, Ap written (24)."""
-    return 12 * nnz + 4 * (n + 1) + (48 if fused else 16) * n
+def csr_spmv_bytes(n: int, nnz: int) -> int:
+    """CSR-priced bytes of one k_spmv_dot launch: val 8 + col 4 per entry,
+    rowptr 4 per row, p read 8 and Ap written 8 per row."""
+    return 12 * nnz + 4 * (n + 1) + 16 * n
 
 
-def parse():
+def update_bytes_per_iter(n: int, mode: int) -> int:
+    """Compulsory bytes of the two vector kernels of one body.
+    k_update_r: r, Ap read, r written (24 n). The x/p update: mode 1 reads x,
+    p, r and writes x, p (40 n); mode 3 (default) writes p_{k+1} from r, p_k
+    (24 n) in three bodies of four and in the fourth also applies
+    x += a0 p0 + .. + a3 p3 (reads x and the three other p buffers, writes x:
+    +40 n), 34 n on average."""
+    xp = 40 * n if mode == 1 else 34 * n
+    return 24 * n + xp
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--grid", type=int, default=256,
-                    help="n of the n^3 grid per GPU (weak), or of the global grid (--strong)")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: one global n^3 grid split into z-slabs over the GPUs "
-                         "(e.g. --grid 512, SURVEY §8(e)); default is weak scaling")
+                    help="n of the global n^3 grid (strong scaling, the default), or of each "
+                         "rank's slab with --weak")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: every rank owns an n^3 slab of an n x n x (n N) grid")
+    ap.add_argument("--strong", action="store_true", help=argparse.SUPPRESS)  # the default
     ap.add_argument("--poll", type=int, default=64, help="iterations per host poll")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every core this job may use)")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip the csr_general block (general-value formats)")
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
     ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
                          "2 fused (single GPU), 3 three kernels with the x update deferred")
-    ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
-                    help="N>1 collectives: RCCL (default) or the host-staged test transport "
-                         "(lets ranks share one GPU; rehearsal only, numbers meaningless)")
-    return ap.parse_args()
+    ap.add_argument("--transport", choices=["auto", "rccl", "peer", "host"], default="auto",
+                    help="N>1 collectives: auto (device peer transport over xGMI when its "
+                         "self-test passes, else RCCL), rccl, peer (fail if unavailable), or "
+                         "host (host-staged test transport: lets ranks share one GPU; "
+                         "rehearsal only, numbers meaningless)")
+    ap.add_argument("--master-port", type=int, default=0, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher: `bench.py --gpus N` outside torch.distributed.run
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(args, argv) -> list[str]:
+    """The torch.distributed.run command line that starts args.gpus ranks of
+    this script with the same arguments (rendezvous on 127.0.0.1)."""
+    port = args.master_port or _free_port()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+            f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(args, argv) -> int | None:
+    """Start the ranks as a child process when --gpus N > 1 and no launcher
+    environment exists (nothing has touched a GPU yet: the parent never
+    initialises HIP). Returns the child's exit code, or None to run here."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus <= 1:
+            return None
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return subprocess.call(launcher_cmd(args, argv), env=env)
+    if int(world) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: they must match")
+    return None
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------
+def job_cores() -> dict:
+    """Cores this job may run on: the affinity mask, capped by a cgroup CPU
+    quota and by the job's declared CPU share (OMP_NUM_THREADS) when set;
+    plus nproc and the CPU model for the record."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        pass
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    use = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    # the GPU box declares this job's CPU share in OMP_NUM_THREADS (16 per
+    # GPU; nproc there counts the whole machine): stay within it
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        use = min(use, int(share))
+    return {"use": int(use), "affinity": int(aff), "cgroup_quota": quota,
+            "declared_share": int(share) if share and share.isdigit() else None,
+            "nproc": os.cpu_count(), "model": model}
 
 
 def cpu_baseline(n3: int, threads: int, budget_s: float):
     """The oracle's OpenMP restatement of the reference iteration on a sample
     of the same workload (same matrix, same b), timed on host cores."""
+    import numpy as np
     from oracle import oracle as O
 
+    info = job_cores()
+    if threads <= 0:
+        threads = info["use"]
     rp, cl, vl = O.poisson(3, n3, n3, n3)
     n, nnz = len(rp) - 1, len(vl)
     b = np.arange(1, n + 1, dtype=np.float64)
-    t1, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, 1, threads)  # probe one iteration
-    iters = max(1, min(5000, int(budget_s / max(t1, 1e-6))))  # ~budget_s of CPU work
+    t1, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, 2, threads)  # probe (also warms the pool)
+    iters = max(1, min(5000, int(budget_s / max(t1 / 2, 1e-6))))  # ~budget_s of CPU work
     t, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, iters, threads)
     its = iters / t
     return {
@@ -104,27 +202,43 @@ def cpu_baseline(n3: int, threads: int, budget_s: float):
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "iterations_per_s": round(its, 3),
+        "host": {"cpu_model": info["model"], "nproc": info["nproc"],
+                 "affinity_cores": info["affinity"], "cgroup_cpu_quota": info["cgroup_quota"],
+                 "declared_cpu_share": info["declared_share"],
+                 "omp_proc_bind": os.environ.get("OMP_PROC_BIND")},
         "sample": f"{n3}^3 7-pt Poisson, {iters} iterations of the reference command "
-                  f"sequence (oracle/cg_oracle.c orc_cg_fixed_iters_omp, OpenMP), "
-                  f"{its:.3f} it/s, {t:.2f} s",
+                  f"sequence (oracle/cg_oracle.c orc_cg_fixed_iters_omp, OpenMP, "
+                  f"{threads} threads), {its:.3f} it/s, {t:.2f} s; value priced at the "
+                  f"CSR bytes B_alg",
     }
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+# the measured run (one rank)
+# ---------------------------------------------------------------------------
+def run(args) -> None:
+    import numpy as np
+    import torch  # noqa: F401  (before libcgx: one HIP runtime per process)
+    import torch.distributed as dist
+
+    import conjugategradient_amd as cga
+    from conjugategradient_amd._native import F64, check, lib
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
-    dev = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(dev)
+    dev = local % max(1, cga.device_count())
     L = lib()
     q = cga.Queue(dev)
     n3 = args.grid
-    if args.strong:
+    strong = not args.weak
+    if strong:
         if n3 % world:
-            raise SystemExit(f"--strong needs the grid ({n3}) divisible by the GPU count ({world})")
+            raise SystemExit(f"strong scaling needs the grid ({n3}) divisible by the GPU "
+                             f"count ({world})")
         nz_global = n3
         n_local = n3 * n3 * (n3 // world)
     else:
@@ -133,11 +247,13 @@ def main():
     row_begin = rank * n_local
     n_global = n_local * world
 
-    # ---- RCCL communicator (N > 1) ---------------------------------------
+    # ---- communicator (N > 1) ----------------------------------------------
+    transport = "single"
     if world > 1 and args.transport == "host":
         from conjugategradient_amd.hostcomm import HostTransport
-        transport = HostTransport()
-        transport.attach(q)
+        ht = HostTransport()
+        ht.attach(q)
+        transport = "host"
     elif world > 1:
         uid = C.create_string_buffer(128)
         if rank == 0:
@@ -145,8 +261,14 @@ def main():
         obj = [bytes(uid.raw) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         check(L.cgx_dist_init(q.handle, rank, world, obj[0], 128))
+        transport = "rccl"
+    wr, ww = C.c_int(0), C.c_int(0)
+    check(L.cgx_dist_rank(q.handle, C.byref(wr), C.byref(ww)))
+    if ww.value != args.gpus or ww.value != world:
+        raise SystemExit(f"bench.py: communicator world {ww.value}, --gpus {args.gpus}, "
+                         f"WORLD_SIZE {world}: they must match")
 
-    # ---- inputs generated in HBM -------------------------------------------
+    # ---- inputs generated in HBM ---------------------------------------------
     nnz_local = L.cgx_poisson_nnz(3, n3, n3, nz_global, row_begin, row_begin + n_local)
     nnz_global = L.cgx_poisson_nnz(3, n3, n3, nz_global, 0, n_global)
     rows = cga.DeviceArray(q, n_local + 1, np.int32)
@@ -165,20 +287,33 @@ def main():
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
                                None, C.byref(A)))
+    if world > 1 and transport == "rccl" and args.transport in ("auto", "peer"):
+        # device peer transport over xGMI: verified by a self-test on every
+        # rank; all ranks agree on the outcome (else RCCL stays)
+        ok = C.c_int(0)
+        rc = L.cgx_dist_peer_enable(A, C.byref(ok)) if hasattr(L, "cgx_dist_peer_enable") else 1
+        if rc == 0 and ok.value:
+            transport = "peer"
+        elif args.transport == "peer":
+            raise SystemExit(f"bench.py: peer transport unavailable: "
+                             f"{L.cgx_last_error().decode()}")
     variant = C.c_int(0)
     check(L.cgx_csr_variant(A, C.byref(variant)))
+    sbytes = C.c_int64(0)
+    check(L.cgx_csr_stream_bytes(A, C.byref(sbytes)))
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
     check(L.cgx_cg_set_mode(cg, args.mode))
     fused = args.mode == 2
+    mode_eff = 3 if args.mode == 0 else args.mode
     total = args.warmup + args.steps + args.profile_steps
     check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total))
     bodies, stopped = C.c_int64(0), C.c_int(0)
     if args.warmup:
         check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
 
-    # ---- timed region --------------------------------------------------------
+    # ---- timed region ----------------------------------------------------------
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -199,9 +334,21 @@ def main():
     if ran != args.steps:
         raise RuntimeError(f"ran {ran} iterations, expected {args.steps} (stopped={stopped.value})")
     its = args.steps / elapsed
-    value = b_alg(n_global, nnz_global) * its / 1e9
 
-    # ---- per-kernel HIP-event pass (roofline) ---------------------------------
+    # compulsory bytes of one iteration in the streamed formats, all ranks
+    spmv_fmt_local = sbytes.value + 16 * n_local  # matrix stream + p read + Ap written
+    iter_local = spmv_fmt_local + update_bytes_per_iter(n_local, mode_eff)
+    if fused:
+        iter_local = sbytes.value + 48 * n_local + 24 * n_local
+    iter_global = iter_local
+    if world > 1:
+        tb = torch.tensor([float(iter_local)], dtype=torch.float64)
+        dist.all_reduce(tb)
+        iter_global = int(tb.item())
+    value = iter_global * its / 1e9
+    csr_eq = b_alg(n_global, nnz_global) * its / 1e9
+
+    # ---- per-kernel HIP-event pass (roofline) ------------------------------------
     avg = (C.c_double * 4)()
     calls = (C.c_int64 * 4)()
     roof = None
@@ -211,30 +358,27 @@ def main():
         check(L.cgx_cg_kernel_times(cg, avg, calls))
         check(L.cgx_cg_set_kernel_timing(cg, 0))
     if calls[1] > 0:
-        kb = spmv_dot_bytes(n_local, nnz_local, fused)
+        kb = spmv_fmt_local + (32 * n_local if fused else 0)
         ach = kb / (avg[1] * 1e-3) / 1e9
+        cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_spmv_fused" if fused else "k_spmv_dot", "bytes_per_launch": kb,
+                "kernel": "k_spmv_fused" if fused else "k_spmv_dot",
+                "bytes_per_launch": kb,
+                "bytes_basis": "compulsory bytes of the kernel's own format: matrix stream "
+                               "(cgx_csr_stream_bytes) + p read + Ap written",
                 "avg_us": round(avg[1] * 1e3, 2), "launches_timed": int(calls[1]),
+                "csr_equivalent_bytes_per_launch": cb,
+                "csr_equivalent_GBs": round(cb / (avg[1] * 1e-3) / 1e9, 1),
                 "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2)}}
-        # the same launch priced at the bytes its storage format streams (the
-        # SELL-P / value-code copy is smaller than CSR, so `frac` on CSR bytes
-        # can exceed 1)
-        sb = C.c_int64(0)
-        check(L.cgx_csr_stream_bytes(A, C.byref(sb)))
-        fb = sb.value + (kb - (12 * nnz_local + 4 * (n_local + 1)))
-        fach = fb / (avg[1] * 1e-3) / 1e9
-        roof.update({"format_bytes_per_launch": fb, "format_achieved": round(fach, 1),
-                     "format_frac": round(fach / HBM_PEAK_GBS, 4)})
         if not fused:
-            roof["other_kernels_avg_us"]["k_update_xp"] = round(avg[3] * 1e3, 2)
+            roof["other_kernels_avg_us"]["k_update_p"] = round(avg[3] * 1e3, 2)
         pmc = os.path.join(ROOT, "profiles", "pmc_spmv_dot.json")
         if os.path.exists(pmc):
             try:
                 meta = json.load(open(pmc))
                 # PMC bytes of this very kernel: same per-GPU grid, variant, mode
-                if (meta.get("grid") == n3 and not args.strong
+                if (meta.get("grid") == n3 and world == 1
                         and meta.get("spmv_variant") == variant.value
                         and meta.get("kernel") == roof["kernel"]):
                     roof["traffic"] = meta.get("hbm_bytes_per_launch")
@@ -242,13 +386,22 @@ def main():
             except Exception:
                 pass
 
+    # ---- general-value formats on the same matrix (N = 1) --------------------------
+    general = None
+    if world == 1 and rank == 0 and not args.no_general:
+        general = general_formats(L, q, A, b, x, n_local, nnz_local, mode_eff, args)
+
+    line = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu and n3 <= 256:
-            cpu = cpu_baseline(n3, min(args.cpu_threads, os.cpu_count() or 1), args.cpu_budget_s)
+            os.environ.setdefault("OMP_PROC_BIND", "close")
+            cpu = cpu_baseline(n3, args.cpu_threads, args.cpu_budget_s)
+        workload = (f"3D 7-pt Poisson {n3}^3 global, {nz_global // world} z-planes per GPU"
+                    if strong else
+                    f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x{nz_global})")
         line = {
-            "metric": "CG iterations/sec + achieved HBM GB/s, 256³ 7-pt Poisson fp64, "
-                      "1/2/4/8 GPUs",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -257,32 +410,99 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "iterations_per_s": round(its, 2),
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (3-D 7-point Dirichlet Poisson CSR generated in HBM, "
                     "b_i = i + 1, x0 = 0)",
-            "config": {"workload": (f"3D 7-pt Poisson {n3}^3 global, {nz_global // world} z-planes "
-                                    f"per GPU" if args.strong else
-                                    f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x"
-                                    f"{nz_global})") + ", CSR fp64/int32 input, SpMV in the "
-                                   "per-matrix best format",
+            "value_basis": "compulsory HBM bytes per iteration in the streamed formats "
+                           "(all ranks) x iterations/s",
+            "bytes_per_iteration": iter_global,
+            "iteration_frac": round(value / (HBM_PEAK_GBS * world), 4),
+            "csr_equivalent_GBs": round(csr_eq, 2),
+            "csr_equivalent_bytes_per_iteration": b_alg(n_global, nnz_global),
+            "config": {"workload": workload + ", CSR fp64/int32 input, SpMV in the "
+                                              "per-matrix best format",
                        "rows_global": n_global, "nnz_global": nnz_global,
-                       "bytes_per_iteration": b_alg(n_global, nnz_global),
                        "parallelism": f"rows{world}" if world > 1 else "single",
+                       "transport": transport,
                        "iteration": {0: "3 kernels, x update deferred over 4 bodies (auto)",
                                      1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies"}[args.mode],
                        "spmv_variant": int(variant.value)},
             "roofline": roof,
+            "csr_general": general,
             "cpu_baseline": cpu,
         }
+    check(L.cgx_cg_destroy(cg))
+    check(L.cgx_csr_destroy(A))
+    if line is not None:
         print(json.dumps(line), flush=True)
-    lib().cgx_cg_destroy(cg)
-    lib().cgx_csr_destroy(A)
     if world > 1:
         dist.destroy_process_group()
 
 
+def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):
+    """The same matrix with value codes off: plain SELL-P (8 B of value per
+    slot, the format of a banded matrix with many distinct values) and
+    CSR-stream (the general CSR kernel: any sparsity, e.g. G3_circuit).
+    Per format: iterations/s over `steps` graph-replayed bodies, and the
+    SpMV's HIP-event time priced at its own format's compulsory bytes."""
+    from conjugategradient_amd._native import check
+
+    out = {}
+    orig = C.c_int(0)
+    check(L.cgx_csr_variant(A, C.byref(orig)))
+    for name, req in (("sellp_plain", 8194), ("csr_stream", 15)):
+        try:
+            check(L.cgx_csr_set_variant(A, req))
+        except Exception as e:  # the matrix lacks the layout
+            out[name] = {"error": str(e)}
+            continue
+        v = C.c_int(0)
+        check(L.cgx_csr_variant(A, C.byref(v)))
+        sb = C.c_int64(0)
+        check(L.cgx_csr_stream_bytes(A, C.byref(sb)))
+        cg = C.c_void_p()
+        check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+        check(L.cgx_cg_config(cg, args.poll, 1))
+        check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 10 + steps + prof))
+        bodies, stopped = C.c_int64(0), C.c_int(0)
+        check(L.cgx_cg_run(cg, 10, C.byref(bodies), C.byref(stopped)))
+        q.wait()
+        t0 = time.perf_counter()
+        check(L.cgx_cg_run(cg, steps, C.byref(bodies), C.byref(stopped)))
+        q.wait()
+        t1 = time.perf_counter()
+        avg = (C.c_double * 4)()
+        calls = (C.c_int64 * 4)()
+        check(L.cgx_cg_set_kernel_timing(cg, 1))
+        check(L.cgx_cg_run(cg, prof, C.byref(bodies), C.byref(stopped)))
+        check(L.cgx_cg_kernel_times(cg, avg, calls))
+        check(L.cgx_cg_destroy(cg))
+        its = steps / (t1 - t0)
+        kb = sb.value + 16 * n
+        it_b = kb + update_bytes_per_iter(n, mode_eff)
+        out[name] = {"spmv_variant": int(v.value), "iterations_per_s": round(its, 2),
+                     "GBs": round(it_b * its / 1e9, 1),
+                     "iteration_frac": round(it_b * its / 1e9 / HBM_PEAK_GBS, 4),
+                     "spmv_avg_us": round(avg[1] * 1e3, 2), "spmv_bytes_per_launch": kb,
+                     "spmv_frac": round(kb / (avg[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "csr_equivalent_spmv_frac": round(
+                         csr_spmv_bytes(n, nnz) / (avg[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    check(L.cgx_csr_set_variant(A, orig.value))
+    return out
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = maybe_launch(args, argv)
+    if rc is not None:
+        return rc
+    run(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -153,9 +153,9 @@ class Matrix:
         return m
 
     def _drop_schedule(self):
-        # a closed queue has already released the context the handle points
-        # into (interpreter shutdown, or a fixture closing the queue first)
-        if self._csr and self._queue.handle:
+        # libcgx refcounts the context from the handle, so this is valid after
+        # the queue was closed (interpreter shutdown, a fixture closing first)
+        if self._csr:
             lib().cgx_csr_destroy(self._csr)
         self._csr = None
 
@@ -405,7 +405,7 @@ class CG:
 
     # -- solve ----------------------------------------------------------
     def _drop_solver(self):
-        if self._cg and self._queue.handle:  # see Matrix._drop_schedule
+        if self._cg:  # valid after Queue.close (see Matrix._drop_schedule)
             lib().cgx_cg_destroy(self._cg)
         self._cg = None
         self._cg_for = None

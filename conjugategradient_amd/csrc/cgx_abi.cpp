@@ -405,8 +405,31 @@ extern "C" int cgx_create(int device, cgx_ctx **out) {
   return CGX_OK;
 }
 
+void cgx::ctx_retain(cgx_ctx *ctx) { ctx->refs.fetch_add(1, std::memory_order_relaxed); }
+
+static void ctx_free(cgx_ctx *ctx);
+
+void cgx::ctx_release(cgx_ctx *ctx) {
+  if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) ctx_free(ctx);
+}
+
+void cgx::csr_retain(cgx_csr *A) { A->refs.fetch_add(1, std::memory_order_relaxed); }
+
+static void csr_free(cgx_csr *A);
+
+void cgx::csr_release(cgx_csr *A) {
+  if (A->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) csr_free(A);
+}
+
+// The owner's release: the context lives on while matrices or solvers made
+// on it do (the last of them frees it).
 extern "C" int cgx_destroy(cgx_ctx *ctx) {
   if (!ctx) return CGX_OK;
+  ctx_release(ctx);
+  return CGX_OK;
+}
+
+static void ctx_free(cgx_ctx *ctx) {
   DeviceGuard g(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   dist_comm_destroy(ctx);
@@ -419,7 +442,6 @@ extern "C" int cgx_destroy(cgx_ctx *ctx) {
   }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
-  return CGX_OK;
 }
 
 extern "C" int cgx_sync(cgx_ctx *ctx) {
@@ -612,6 +634,7 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = h_rowptr[rb[i]];
   auto *A = new cgx_csr();
   A->ctx = ctx;
+  ctx_retain(ctx);
   A->dtype = dtype;
   A->max_row_nnz = mx;
   A->dev = CsrDev{n, nnz, d_rowptr, d_col, d_val, nullptr, nullptr, (int)nrb1 - 1, kTile};
@@ -637,16 +660,25 @@ extern "C" int cgx_csr_create(cgx_ctx *ctx, int64_t n, int64_t nnz, const int *d
   return CGX_OK;
 }
 
+// The owner's release: a solver made on the matrix keeps it alive.
 extern "C" int cgx_csr_destroy(cgx_csr *A) {
   if (!A) return CGX_OK;
-  DeviceGuard g(A->ctx->device);
-  (void)hipStreamSynchronize(A->ctx->stream);
-  if (A->d_rb) (void)hipFree(A->d_rb);
-  if (A->d_ext) (void)hipFree(A->d_ext);
-  free_sell(A);
-  dist_destroy_halo(A);
-  delete A;
+  csr_release(A);
   return CGX_OK;
+}
+
+static void csr_free(cgx_csr *A) {
+  cgx_ctx *ctx = A->ctx;
+  {
+    DeviceGuard g(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (A->d_rb) (void)hipFree(A->d_rb);
+    if (A->d_ext) (void)hipFree(A->d_ext);
+    free_sell(A);
+    dist_destroy_halo(A);
+  }
+  delete A;
+  ctx_release(ctx);
 }
 
 // Rebuild the row-block schedule for another tile size (2048 or 1024).
@@ -1243,7 +1275,10 @@ static bool known_variant(int v) {
                            821248, 821250, 1607680, 1607682, 1869824, 1869826};
   for (int k : ok)
     if (k == v) return true;
-  return false;
+  // the resolved SELL-P forms cgx_csr_variant reports (e.g. 1875970) are
+  // accepted back as requests
+  constexpr int sellp_bits = 8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2;
+  return (v & 8192) && !(v & ~sellp_bits);
 }
 
 extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
@@ -1267,8 +1302,15 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
 // SELL copy is freed when a CSR-stream variant wins.
 int autotune_spmv(cgx_csr *A) {
   if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
-    A->dev.variant = std::atoi(env);
-    if (!(A->dev.variant & (2048 | 8192))) free_sell(A);
+    // the same checks as cgx_csr_set_variant: a mistyped value fails here,
+    // not later as a kernel launch error
+    const int v = std::atoi(env);
+    if (cgx_csr_set_variant(A, v) != CGX_OK) {
+      const std::string why = g_err;
+      set_error("$CGX_SPMV_VARIANT=%s: %s", env, why.c_str());
+      return CGX_EINVAL;
+    }
+    if (!(v & (2048 | 8192))) free_sell(A);
     return CGX_OK;
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
@@ -1466,6 +1508,8 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
   auto *cg = new cgx_cg();
   cg->ctx = ctx;
   cg->A = A;
+  ctx_retain(ctx);
+  csr_retain(A);
   cg->dtype = A->dtype;
   cg->n = A->dev.n;
   const size_t es = dtype_size(cg->dtype);
@@ -1544,7 +1588,11 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
   for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2]})
     if (p) (void)hipFree(p);
+  cgx_csr *A = cg->A;
+  cgx_ctx *ctx = cg->ctx;
   delete cg;
+  csr_release(A);
+  ctx_release(ctx);
   return CGX_OK;
 }
 

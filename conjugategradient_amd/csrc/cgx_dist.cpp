@@ -436,6 +436,7 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   if ((rc = comm_allgather(ctx, recv_cnt.data(), world * sizeof(int64_t), cmat.data()))) return rc;
   auto *A = new cgx_csr();
   A->ctx = ctx;
+  ctx_retain(ctx);
   A->dtype = dtype;
   A->dist = true;
   A->n_global = n_global;

@@ -1464,7 +1464,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (j < K || (j > K + 2 && j < WW)) {
-          const auto g = x.pair_b(rb + (unsigned)(o[j] * (int)sizeof(T)));
+          const auto g = x.pair_b(rb + (unsigned)o[j] * (unsigned)sizeof(T));
           g0[j] = g.x;
           g1[j] = g.y;
         } else if (j >= WW) {
@@ -1498,7 +1498,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
           g0[j] = T(rb & 1);
           g1[j] = T(rb & 2);
         } else {
-          const auto g = x.pair_b(rb + (unsigned)(o[j] * (int)sizeof(T)));
+          const auto g = x.pair_b(rb + (unsigned)o[j] * (unsigned)sizeof(T));
           g0[j] = g.x;
           g1[j] = g.y;
         }

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <string>
@@ -60,7 +61,12 @@ struct HostComm {
 
 }  // namespace cgx
 
+// Lifetime: a context is referenced by its owner (cgx_create .. cgx_destroy)
+// and by every cgx_csr / cgx_cg made on it; a matrix by its owner and by every
+// solver made on it. The last release frees the object, so handles may be
+// destroyed in any order (cgx_destroy before cgx_csr_destroy is valid).
 struct cgx_ctx {
+  std::atomic<int> refs{1};
   int device = 0;
   hipStream_t stream = nullptr;
   void *ws = nullptr;           // cgx::RedWs<double> (large enough for float)
@@ -77,6 +83,7 @@ struct cgx_ctx {
 };
 
 struct cgx_csr {
+  std::atomic<int> refs{1};
   cgx_ctx *ctx = nullptr;
   cgx::CsrDev dev{};
   int dtype = CGX_F64;
@@ -138,6 +145,12 @@ struct cgx_cg {
 };
 
 namespace cgx {
+// reference counts (cgx_abi.cpp): retain on a handle made from the object,
+// release when that handle (or the owner) lets go; the last release frees
+void ctx_retain(cgx_ctx *ctx);
+void ctx_release(cgx_ctx *ctx);
+void csr_retain(cgx_csr *A);
+void csr_release(cgx_csr *A);
 // cgx_dist.cpp
 int dist_halo_exchange(cgx_csr *A, void *d_vec_ext, hipStream_t s);
 // Overlapped form: pack on s, exchange on the context's comm stream (RCCL,

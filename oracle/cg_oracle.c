@@ -356,3 +356,65 @@ double orc_cg_fixed_iters_omp(int64_t n, const int *rowptr, const int *col,
   free(helper); free(r); free(rnext); free(p);
   return t1 - t0;
 }
+
+/* orc_cg_solve on OpenMP threads (full-size parity tests at 16.8 M rows):
+ * the same statements as orc_cg_solve / CG.hpp:314-436 in submission order,
+ * stop rule Q5 (old rxr tested after the x update, NaN stops, cap N+1 or
+ * max_iter), with each parallel_for an OpenMP loop and each dot an OpenMP
+ * reduction (its summation order differs from orc_cg_solve's index order;
+ * every other value is rounded identically). x starts at 0. */
+int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
+                     const double *val, const double *b, double *x,
+                     double tol, int64_t max_iter, int threads,
+                     orc_cg_result *res) {
+  omp_set_num_threads(threads > 0 ? threads : 1);
+  double *helper = (double *)malloc((size_t)n * sizeof(double));
+  double *rnext = (double *)malloc((size_t)n * sizeof(double));
+  double *p = (double *)malloc((size_t)n * sizeof(double));
+  if (!helper || !rnext || !p) { free(helper); free(rnext); free(p); return 3; }
+  double rxr = 0;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    x[i] = 0;
+    rnext[i] = b[i]; /* r = b - A 0 (CG.hpp:324-332) */
+    p[i] = rnext[i];
+  }
+#pragma omp parallel for schedule(static) reduction(+ : rxr)
+  for (int64_t i = 0; i < n; ++i) rxr += rnext[i] * rnext[i];
+  if (res) res->rxr0 = rxr;
+  int64_t counter = 0, bodies = 0;
+  int done = 0;
+  do {
+    double value2 = 0, value3 = 0, alpha, beta;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {                             /* :374-375 */
+      double s = 0;
+      for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) s += val[j] * p[col[j]];
+      helper[i] = s;
+    }
+#pragma omp parallel for schedule(static) reduction(+ : value2)
+    for (int64_t i = 0; i < n; ++i) value2 += helper[i] * p[i];   /* :378-379 */
+    alpha = rxr / value2;                                         /* :385-386 */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      x[i] = x[i] + alpha * p[i];                                 /* :390 */
+      rnext[i] = rnext[i] - alpha * helper[i];                    /* :392-393 */
+    }
+    if (isnan(rxr) || sqrt(rxr) <= tol) done = 1;                 /* :400-403 */
+#pragma omp parallel for schedule(static) reduction(+ : value3)
+    for (int64_t i = 0; i < n; ++i) value3 += rnext[i] * rnext[i];/* :406-407 */
+    beta = value3 / rxr;                                          /* :414 */
+    rxr = value3;                                                 /* :415 */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) p[i] = rnext[i] + beta * p[i];/* :418 */
+    ++bodies;
+    if (max_iter >= 0 && bodies >= max_iter) break;
+  } while ((uint64_t)(counter++) < (uint64_t)n && !done);        /* :436 */
+  if (res) {
+    res->iterations = bodies;
+    res->rxr = rxr;
+    res->stopped_by_tol = done;
+  }
+  free(helper); free(rnext); free(p);
+  return 0;
+}

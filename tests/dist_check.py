@@ -35,6 +35,11 @@ from conjugategradient_amd._native import F64, check, lib  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--nxy", type=int, default=0,
+                    help="nx = ny of the global grid (0: --grid); nz stays --grid")
+    ap.add_argument("--bodies", type=int, default=-1,
+                    help="fixed body count at tol 0, checked against the oracle's OpenMP "
+                         "iteration (for large grids); -1: solve to --tol")
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl")
     ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3)")
@@ -58,17 +63,18 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         check(L.cgx_dist_init(q.handle, rank, world, obj[0], 128))
     g = a.grid
-    n = g * g * g
+    gxy = a.nxy or g
+    n = gxy * gxy * g
     base, extra = divmod(n, world)
     counts = [base + (r < extra) for r in range(world)]
     begin = sum(counts[:rank])
     nl = counts[rank]
-    nnz = L.cgx_poisson_nnz(3, g, g, g, begin, begin + nl)
+    nnz = L.cgx_poisson_nnz(3, gxy, gxy, g, begin, begin + nl)
     rows = cga.DeviceArray(q, nl + 1, np.int32)
     cols = cga.DeviceArray(q, nnz, np.int32)
     vals = cga.DeviceArray(q, nnz, np.float64)
-    check(L.cgx_poisson_fill(q.handle, F64, 3, g, g, g, begin, begin + nl, rows.ptr, cols.ptr,
-                             vals.ptr))
+    check(L.cgx_poisson_fill(q.handle, F64, 3, gxy, gxy, g, begin, begin + nl, rows.ptr,
+                             cols.ptr, vals.ptr))
     A = C.c_void_p()
     check(L.cgx_csr_create_dist(q.handle, n, begin, nl, nnz, rows.ptr, cols.ptr, vals.ptr, F64,
                                 C.byref(A)))
@@ -84,24 +90,42 @@ def main():
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_set_mode(cg, a.mode))
     bodies, rxr = C.c_int64(), C.c_double()
-    check(L.cgx_cg_solve(cg, b.ptr, x.ptr, a.tol, -1, C.byref(bodies), C.byref(rxr)))
+    tol = 0.0 if a.bodies >= 0 else a.tol
+    check(L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, a.bodies, C.byref(bodies), C.byref(rxr)))
     acc = C.c_double()
     check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
     parts = [None] * world
-    dist.all_gather_object(parts, (x.download().tolist(), int(ghosts.value), int(nbrs.value),
-                                   (ni.value, nb.value)))
+    dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value)))
+    # x to rank 0 as tensors, padded to the largest block (gloo gathers
+    # equal sizes; blocks differ by at most one row)
+    mx = max(counts)
+    xl = torch.zeros(mx, dtype=torch.float64)
+    xl[:nl] = torch.from_numpy(x.download())
+    xs = [torch.empty(mx, dtype=torch.float64) for _ in counts] if rank == 0 else None
+    if world > 1:
+        dist.gather(xl, xs, dst=0)
+    else:
+        xs = [xl]
     if rank == 0:
         from oracle import oracle as O
-        xg = np.concatenate([np.array(p[0]) for p in parts])
-        rp, cl, vl = O.poisson(3, g, g, g)
-        xr, res = O.cg_solve(rp, cl, vl, np.arange(1, n + 1, dtype=np.float64), a.tol)
+        xg = torch.cat([t[:c] for t, c in zip(xs, counts)]).numpy()
+        rp, cl, vl = O.poisson(3, gxy, gxy, g)
+        bg = np.arange(1, n + 1, dtype=np.float64)
+        if a.bodies >= 0:
+            _, xr = O.cg_fixed_iters_omp(rp, cl, vl, bg, a.bodies, 16)
+            oracle_bodies = a.bodies
+        else:
+            xr, res = O.cg_solve(rp, cl, vl, bg, a.tol)
+            oracle_bodies = res.iterations
         relerr = float(np.linalg.norm(xg - xr) / np.linalg.norm(xr))
-        ok = relerr <= 1e-10 and abs(bodies.value - res.iterations) <= 2
-        print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode, "grid": g, "bodies": bodies.value,
-                          "oracle_bodies": res.iterations, "rel_err": relerr,
-                          "accuracy": acc.value, "ghosts": [p[1] for p in parts],
-                          "neighbours": [p[2] for p in parts],
-                          "split": [p[3] for p in parts], "ok": ok}), flush=True)
+        ok = bool(relerr <= 1e-10 and abs(bodies.value - oracle_bodies) <= 2
+                  and np.isfinite(xg).all())
+        print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode,
+                          "grid": [gxy, gxy, g], "bodies": bodies.value,
+                          "oracle_bodies": oracle_bodies, "rel_err": relerr,
+                          "accuracy": acc.value, "ghosts": [p[0] for p in parts],
+                          "neighbours": [p[1] for p in parts],
+                          "split": [p[2] for p in parts], "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)
     L.cgx_csr_destroy(A)
     q.close()

@@ -1,0 +1,62 @@
+"""bench.py's host logic (no GPU): argument handling, the N-rank launcher,
+and the byte accounting behind `value`, `roofline` and `csr_equivalent_GBs`."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_defaults_are_strong_scaling_of_256():
+    a = bench.parse([])
+    assert a.gpus == 1 and a.grid == 256 and not a.weak and a.transport == "auto"
+    assert bench.parse(["--weak"]).weak
+
+
+def test_launcher_starts_n_ranks(monkeypatch):
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    argv = ["--gpus", "4", "--steps", "9", "--grid", "512"]
+    assert bench.main(argv) == 7  # the child's exit code is the parent's
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[cmd.index(os.path.join(ROOT, "bench.py")) + 1:] == argv
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_single_gpu_runs_in_process(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.maybe_launch(bench.parse([]), []) is None
+
+
+def test_world_size_must_match_gpus(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="must match"):
+        bench.maybe_launch(bench.parse(["--gpus", "4"]), ["--gpus", "4"])
+    assert bench.maybe_launch(bench.parse(["--gpus", "2"]), ["--gpus", "2"]) is None
+
+
+def test_byte_accounting():
+    n, nnz = 256 ** 3, 117_047_296
+    assert bench.b_alg(n, nnz) == 2_813_853_700  # 2.8139 GB
+    assert bench.csr_spmv_bytes(n, nnz) == 12 * nnz + 4 * (n + 1) + 16 * n
+    # r update 24 n; x/p update 40 n (mode 1) or 34 n averaged (mode 3)
+    assert bench.update_bytes_per_iter(n, 1) == 64 * n
+    assert bench.update_bytes_per_iter(n, 3) == 58 * n
+
+
+def test_job_cores_reports_host():
+    info = bench.job_cores()
+    assert 1 <= info["use"] <= info["affinity"] <= (os.cpu_count() or info["affinity"])
+    assert "model" in info and info["nproc"] == os.cpu_count()

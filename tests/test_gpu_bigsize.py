@@ -1,0 +1,101 @@
+"""The two BASELINE configs beyond 16.8 M rows or without a stencil:
+
+* 512^3 on one GPU (134 M rows, the 8-GPU config's whole problem): the
+  production SpMV format (value-code stencil SELL-P) equals the general
+  CSR-stream kernel bit for bit on the device (both sum each row in CSR
+  order), and the deferred-x iteration (mode 3) equals the three-kernel one
+  (mode 1) bit for bit over 12 bodies — size-independent properties, since
+  the CPU oracle would take minutes per body here.
+* the G3_circuit stand-in at its real size (1,585,478 rows, irregular rows,
+  thousands of distinct values -> CSR-stream): SpMV bit-exact against the
+  oracle, and a solve to a tight relative tolerance held to the bars of
+  test_gpu_kernels.py::test_cg_irregular.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import conjugategradient_amd as cga
+from conjugategradient_amd._native import check, lib
+from tests.util import irregular_spd, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _variant(m):
+    v = C.c_int(0)
+    check(lib().cgx_csr_variant(m.schedule(), C.byref(v)))
+    return v.value
+
+
+def test_512cubed_formats_and_modes_agree(queue):
+    m = cga.Matrix.poisson(queue, 3, 512, 512, 512)
+    n = m.N()
+    assert n == 512 ** 3
+    prod = _variant(m)
+    assert prod & 32768 and prod & 8192, prod  # value-code SELL-P
+    x = np.random.default_rng(512).standard_normal(n)
+    xv = cga.Vector(queue, x)
+    y1, y2 = cga.Vector(queue, n), cga.Vector(queue, n)
+    ops = cga.VectorOperations(queue)
+    ops.spmv(m, xv, y1, m.NNZ(), count=n)
+    check(lib().cgx_csr_set_variant(m.schedule(), 15))  # CSR-stream
+    ops.spmv(m, xv, y2, m.NNZ(), count=n)
+    check(lib().cgx_csr_set_variant(m.schedule(), prod))
+    a1 = y1.to_numpy()
+    np.testing.assert_array_equal(a1, y2.to_numpy())
+    del y1, y2, xv
+    b = np.arange(1, n + 1, dtype=np.float64)
+    xs = []
+    for mode in (3, 1):
+        cg = cga.CG(queue)
+        cg.mode = mode
+        cg.setMatrix(m)
+        cg.setTarget(b)
+        cg.solve(0.0, max_iter=12)
+        assert cg.iterations == 12
+        xs.append(cg.extract())
+        del cg
+    assert np.isfinite(xs[0]).all()
+    np.testing.assert_array_equal(xs[0], xs[1])
+
+
+G3_N = 1_585_478
+
+
+@pytest.fixture(scope="module")
+def g3():
+    return irregular_spd(G3_N, mean_deg=3.83, seed=12345)
+
+
+def test_g3_standin_spmv_bitexact(queue, oracle, g3):
+    rp, cl, vl = g3
+    assert len(rp) - 1 == G3_N
+    m = cga.Matrix(queue, vl, cl, rp)
+    assert not (_variant(m) & 32768)  # too many distinct values for codes
+    x = np.random.default_rng(3).standard_normal(G3_N)
+    y = cga.Vector(queue, G3_N)
+    cga.VectorOperations(queue).spmv(m, cga.Vector(queue, x), y, m.NNZ(), count=G3_N)
+    np.testing.assert_array_equal(y.to_numpy(), oracle.spmv(rp, cl, vl, x))
+
+
+def test_g3_standin_solve_matches_oracle(queue, oracle, g3):
+    # ill-conditioned (shift 1e-2): the body count reacts to the dots'
+    # summation order, so the bars are test_cg_irregular's (5 % of the
+    # bodies, solution 1e-6, residual within 10x of the oracle's)
+    rp, cl, vl = g3
+    b = np.arange(1, G3_N + 1, dtype=np.float64)
+    tol = 1e-10 * float(np.linalg.norm(b))
+    cg = cga.CG(queue)
+    cg.setMatrix(cga.Matrix(queue, vl, cl, rp))
+    cg.setTarget(b)
+    cg.solve(tol)
+    x = cg.extract()
+    xr, res = oracle.cg_solve_omp(rp, cl, vl, b, tol, 16)
+    print("g3 bodies gpu", cg.iterations, "oracle", res.iterations, "rel", rel(x, xr))
+    assert res.stopped_by_tol
+    assert abs(cg.iterations - res.iterations) <= max(2, res.iterations // 20)
+    assert rel(x, xr) <= 1e-6
+    r = oracle.spmv(rp, cl, vl, x) - b
+    assert np.linalg.norm(r) <= 10 * max(np.linalg.norm(oracle.spmv(rp, cl, vl, xr) - b), tol)

@@ -85,3 +85,33 @@ def test_fullsize_cg_bodies_match_oracle(queue, oracle, full):
     # accuracy() (CG.hpp:463-515) of the device x against the oracle's formula
     acc = cg3.accuracy()
     assert acc == pytest.approx(oracle.accuracy(rp, cl, vl, b, x3), rel=1e-9)
+
+
+# ---- the stop rule (Q5) and the end-of-run x flush at production size -------
+# CG.hpp:396-404,436: the body tests the r.r it started with, after its x
+# update; the deferred-x iteration (mode 3) then applies the pending x updates
+# of the last group of four. tol is absolute in the reference (sqrt(rxr) <=
+# tol); these tolerances are chosen relative to ||b||: 1e-8 at 256^3 (about
+# 890 bodies), and 28 ||b|| at 4096^2 (the 2-D residual first GROWS to
+# ~32 ||b|| with b_i = i + 1 and falls slowly: a few hundred bodies; 1e-8 is
+# thousands of bodies away, out of reach of the CPU oracle in a test).
+TOL_REL = {"poisson2d_4096": 28.0, "poisson3d_256": 1e-8}
+
+
+def test_fullsize_solve_to_tolerance_matches_oracle(queue, oracle, full):
+    name, m, (rp, cl, vl) = full
+    n = m.N()
+    b = np.arange(1, n + 1, dtype=np.float64)
+    tol = TOL_REL[name] * float(np.linalg.norm(b))
+    cg = cga.CG(queue)
+    cg.setMatrix(m)
+    cg.setTarget(b)
+    cg.solve(tol)
+    x = cg.extract()
+    xr, res = oracle.cg_solve_omp(rp, cl, vl, b, tol, 16)
+    print(name, "bodies gpu", cg.iterations, "oracle", res.iterations, "rel", rel(x, xr))
+    assert res.stopped_by_tol and 100 < res.iterations < 3000
+    assert abs(cg.iterations - res.iterations) <= 2
+    assert rel(x, xr) <= 1e-10
+    # the stop is the reference's: the final r.r is the body's new one
+    assert cg.final_rxr == pytest.approx(res.rxr, rel=1e-6)
