@@ -362,9 +362,10 @@ double orc_cg_fixed_iters_omp(int64_t n, const int *rowptr, const int *col,
  * stop rule Q5 (old rxr tested after the x update, NaN stops, cap N+1 or
  * max_iter), with each parallel_for an OpenMP loop and each dot an OpenMP
  * reduction (its summation order differs from orc_cg_solve's index order;
- * every other value is rounded identically). x starts at 0. */
+ * every other value is rounded identically). x is in/out as in
+ * orc_cg_solve (zero-filled first when has_x0 == 0). */
 int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
-                     const double *val, const double *b, double *x,
+                     const double *val, const double *b, double *x, int has_x0,
                      double tol, int64_t max_iter, int threads,
                      orc_cg_result *res) {
   omp_set_num_threads(threads > 0 ? threads : 1);
@@ -374,9 +375,14 @@ int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
   if (!helper || !rnext || !p) { free(helper); free(rnext); free(p); return 3; }
   double rxr = 0;
 #pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {                               /* :324-332 */
+    if (!has_x0) x[i] = 0;
+  }
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) {
-    x[i] = 0;
-    rnext[i] = b[i]; /* r = b - A 0 (CG.hpp:324-332) */
+    double s = 0;
+    for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) s += val[j] * x[col[j]];
+    rnext[i] = b[i] - s;
     p[i] = rnext[i];
   }
 #pragma omp parallel for schedule(static) reduction(+ : rxr)

@@ -89,11 +89,11 @@ double orc_cg_fixed_iters_omp(int64_t n, const int *rowptr, const int *col,
                               const double *val, const double *b, double *x,
                               int64_t iters, int threads);
 
-/* orc_cg_solve (x0 = 0) with OpenMP loops and OpenMP-reduction dots: the
- * full-size parity oracle (256^3, 4096^2 to tol 1e-8). Only the dots'
- * summation order differs from orc_cg_solve. */
+/* orc_cg_solve with OpenMP loops and OpenMP-reduction dots: the full-size
+ * parity oracle (16.8 M rows). Only the dots' summation order differs from
+ * orc_cg_solve. */
 int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
-                     const double *val, const double *b, double *x,
+                     const double *val, const double *b, double *x, int has_x0,
                      double tol, int64_t max_iter, int threads,
                      orc_cg_result *res);
 

@@ -68,8 +68,8 @@ def lib() -> C.CDLL:
         L.orc_accuracy.restype = C.c_double
         L.orc_cg_fixed_iters_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [_i64, C.c_int]
         L.orc_cg_fixed_iters_omp.restype = C.c_double
-        L.orc_cg_solve_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [C.c_double, _i64, C.c_int,
-                                                                   C.POINTER(CgResult)]
+        L.orc_cg_solve_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [C.c_int, C.c_double, _i64,
+                                                                   C.c_int, C.POINTER(CgResult)]
         L.orc_cg_solve_omp.restype = C.c_int
         _lib = L
     return _lib
@@ -197,14 +197,15 @@ def cg_fixed_iters_omp(rowptr, col, val, b, iters: int, threads: int):
     return t, x
 
 
-def cg_solve_omp(rowptr, col, val, b, tol: float, threads: int = 16, max_iter: int = -1):
-    """orc_cg_solve on OpenMP threads (x0 = 0): the oracle at 16.8 M rows.
+def cg_solve_omp(rowptr, col, val, b, tol: float, threads: int = 16, max_iter: int = -1,
+                 x0=None):
+    """orc_cg_solve on OpenMP threads: the oracle at 16.8 M rows.
     Returns (x, CgResult)."""
     n = len(rowptr) - 1
-    x = np.zeros(n)
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64, copy=True)
     res = CgResult()
-    rc = lib().orc_cg_solve_omp(n, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(b), _ptr(x), tol,
-                                max_iter, threads, C.byref(res))
+    rc = lib().orc_cg_solve_omp(n, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(b), _ptr(x),
+                                0 if x0 is None else 1, tol, max_iter, threads, C.byref(res))
     if rc:
         raise RuntimeError(f"orc_cg_solve_omp failed: {rc}")
     return x, res
