@@ -102,11 +102,13 @@ def parse(argv=None):
     ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
                          "2 fused (single GPU), 3 three kernels with the x update deferred")
-    ap.add_argument("--transport", choices=["auto", "rccl", "peer", "host"], default="auto",
+    ap.add_argument("--transport", choices=["auto", "rccl", "peer", "host", "host-peer"],
+                    default="auto",
                     help="N>1 collectives: auto (device peer transport over xGMI when its "
-                         "self-test passes, else RCCL), rccl, peer (fail if unavailable), or "
+                         "self-test passes, else RCCL), rccl, peer (fail if unavailable), "
                          "host (host-staged test transport: lets ranks share one GPU; "
-                         "rehearsal only, numbers meaningless)")
+                         "rehearsal only, numbers meaningless), host-peer (host setup, "
+                         "device peer iteration: a one-GPU rehearsal of the peer path)")
     ap.add_argument("--master-port", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -249,7 +251,7 @@ def run(args) -> None:
 
     # ---- communicator (N > 1) ----------------------------------------------
     transport = "single"
-    if world > 1 and args.transport == "host":
+    if world > 1 and args.transport in ("host", "host-peer"):
         from conjugategradient_amd.hostcomm import HostTransport
         ht = HostTransport()
         ht.attach(q)
@@ -287,16 +289,19 @@ def run(args) -> None:
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
                                None, C.byref(A)))
-    if world > 1 and transport == "rccl" and args.transport in ("auto", "peer"):
+    peer_note = None
+    if world > 1 and args.transport in ("auto", "peer", "host-peer"):
         # device peer transport over xGMI: verified by a self-test on every
-        # rank; all ranks agree on the outcome (else RCCL stays)
+        # rank; all ranks agree on the outcome (else the setup transport stays)
         ok = C.c_int(0)
-        rc = L.cgx_dist_peer_enable(A, C.byref(ok)) if hasattr(L, "cgx_dist_peer_enable") else 1
-        if rc == 0 and ok.value:
-            transport = "peer"
-        elif args.transport == "peer":
+        check(L.cgx_dist_peer_enable(A, C.byref(ok)))
+        if ok.value:
+            transport = "peer (setup: " + transport + ")"
+        elif args.transport != "auto":
             raise SystemExit(f"bench.py: peer transport unavailable: "
                              f"{L.cgx_last_error().decode()}")
+        else:
+            peer_note = L.cgx_last_error().decode()
     variant = C.c_int(0)
     check(L.cgx_csr_variant(A, C.byref(variant)))
     sbytes = C.c_int64(0)
@@ -426,6 +431,7 @@ def run(args) -> None:
                        "rows_global": n_global, "nnz_global": nnz_global,
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
+                       "peer_fallback_reason": peer_note,
                        "iteration": {0: "3 kernels, x update deferred over 4 bodies (auto)",
                                      1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies"}[args.mode],

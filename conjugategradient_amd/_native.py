@@ -96,6 +96,8 @@ _SIGS = {
                                    C.POINTER(_vp)]),
     "cgx_csr_halo_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i32)]),
     "cgx_dist_allreduce_sum": (_i32, [_vp, C.POINTER(_dbl)]),
+    "cgx_dist_peer_enable": (_i32, [_vp, C.POINTER(_i32)]),
+    "cgx_dist_peer_info": (_i32, [_vp, C.POINTER(_i32)]),
     # host-only helpers (no device needed)
     "cgx_plan_ghosts": (_i32, [_i64, _i64, _i64, _vp, _i32, _vp, _vp, C.POINTER(_i64),
                                C.POINTER(C.POINTER(_i64)), _vp]),

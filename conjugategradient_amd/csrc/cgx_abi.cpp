@@ -162,6 +162,29 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
   T *Ap = (T *)cg->Ap;
   int rc;
   const bool halo = A->dist && A->halo.n_ghost + A->halo.send_total > 0;
+  if (halo && A->peer.on) {
+    // device peer transport: push p's boundary entries into the neighbours,
+    // run the interior slices, wait for the neighbours' entries, then the
+    // boundary slices (or wait, then one launch when the matrix is not split)
+    if ((rc = peer_push<T>(A, p, st, slot, s))) return rc;
+    const bool split = A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192));
+    const int gi = split ? Launch<T>::slice_grid(A->dev, A->split_ni) : 0;
+    if ((rc = timed(cg, 1, s, [&] {
+           hipError_t e = hipSuccess;
+           if (split)
+             e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
+                                            ws, s, rev);
+           if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
+           if (e == hipSuccess)
+             e = split ? Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,
+                                                    gi, p, Ap, st, slot, ws, s, rev)
+                       : Launch<T>::spmv_dot(A->dev, p, Ap, st, slot, ws, s, rev);
+           return e;
+         })))
+      return rc;
+    *np = split ? gi + Launch<T>::slice_grid(A->dev, A->split_nb) : Launch<T>::spmv_parts(A->dev);
+    return CGX_OK;
+  }
   if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192))) {
     bool async = false;
     if ((rc = dist_halo_post(A, p, s, &async))) return rc;
@@ -188,6 +211,17 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
   return CGX_OK;
 }
 
+// A partitioned run's dot: the local partials summed, then all-reduced into
+// *dst — by the device peer transport in one kernel, or finalized into the
+// scalar ring and all-reduced by the setup transport (RCCL / host).
+template <typename T> int dist_dot(cgx_cg *cg, const T *part, int np, T *dst, int slot) {
+  hipStream_t s = cg->ctx->stream;
+  if (cg->A->peer.on)
+    return peer_allreduce<T>(cg->A, part, np, dst, (CgScalars<T> *)cg->st, slot, s);
+  CGX_HIP(Launch<T>::finalize(part, np, dst, s));
+  return dist_allreduce_scalar(cg->ctx, dst, cg->dtype, 1, s);
+}
+
 template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   cgx_csr *A = cg->A;
   hipStream_t s = cg->ctx->stream;
@@ -203,19 +237,13 @@ template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
   int npp = 0;
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
-  if (A->dist) {
-    CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
-    if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
-  }
+  if (A->dist && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot))) return rc;
   if ((rc = timed(cg, 2, s, [&] {
          return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp,
                                     rpar);
        })))
     return rc;
-  if (A->dist) {
-    CGX_HIP(Launch<T>::finalize(ws->rr_part, npr, &st->rr[slot], s));
-    if ((rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
-  }
+  if (A->dist && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot))) return rc;
   if ((rc = timed(cg, 3, s, [&] {
          return Launch<T>::update_xp(cg->n, x, p, r, st, slot, ws, A->dist ? 0 : npr, s, par);
        })))
@@ -242,19 +270,13 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
   int npp = 0;
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
-  if (A->dist) {
-    CGX_HIP(Launch<T>::finalize(ws->pap_part, npp, &st->pAp[slot], s));
-    if ((rc = dist_allreduce_scalar(cg->ctx, &st->pAp[slot], cg->dtype, 1, s))) return rc;
-  }
+  if (A->dist && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot))) return rc;
   if ((rc = timed(cg, 2, s, [&] {
          return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp,
                                     rpar);
        })))
     return rc;
-  if (A->dist) {
-    CGX_HIP(Launch<T>::finalize(ws->rr_part, npr, &st->rr[slot], s));
-    if ((rc = dist_allreduce_scalar(cg->ctx, &st->rr[slot], cg->dtype, 1, s))) return rc;
-  }
+  if (A->dist && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot))) return rc;
   if ((rc = timed(cg, 3, s, [&] {
          return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, A->dist ? 0 : npr,
                                           s, par);
@@ -351,8 +373,10 @@ int build_graph(cgx_cg *cg, int iters) {
 }
 
 bool graph_ok(const cgx_cg *cg) {
-  // RCCL calls are kept out of captured graphs; timing needs eager launches
-  return cg->use_graph && !cg->timing && !cg->A->dist && cg->poll_every % 4 == 0;
+  // RCCL / host-transport calls are kept out of captured graphs (the peer
+  // transport's iteration is all kernels); timing needs eager launches
+  return cg->use_graph && !cg->timing && (!cg->A->dist || cg->A->peer.on) &&
+         cg->poll_every % 4 == 0;
 }
 
 }  // namespace
@@ -675,6 +699,7 @@ static void csr_free(cgx_csr *A) {
     if (A->d_rb) (void)hipFree(A->d_rb);
     if (A->d_ext) (void)hipFree(A->d_ext);
     free_sell(A);
+    peer_destroy(A);
     dist_destroy_halo(A);
   }
   delete A;
@@ -1628,7 +1653,17 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
     // initial guess with ghost values, staged in the Ap buffer (free at init)
     const size_t es = dtype_size(cg->dtype);
     CGX_HIP(hipMemcpyAsync(cg->Ap, x, (size_t)cg->n * es, hipMemcpyDeviceToDevice, s));
-    if ((rc = dist_halo_exchange(A, cg->Ap, s))) return rc;
+    if (A->peer.on) {
+      rc = cg->dtype == CGX_F32
+               ? peer_push<float>(A, (const float *)cg->Ap, nullptr, 0, s)
+               : peer_push<double>(A, (const double *)cg->Ap, nullptr, 0, s);
+      if (!rc)
+        rc = cg->dtype == CGX_F32 ? peer_wait<float>(A, (float *)cg->Ap, nullptr, 0, s)
+                                  : peer_wait<double>(A, (double *)cg->Ap, nullptr, 0, s);
+    } else {
+      rc = dist_halo_exchange(A, cg->Ap, s);
+    }
+    if (rc) return rc;
     xe = cg->Ap;
   }
   rc = timed(cg, 0, s, [&] {
@@ -1642,7 +1677,17 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
                                    cap, s);
   });
   if (rc) return rc;
-  if (A->dist) {
+  if (A->dist && A->peer.on) {
+    // the init kernel left the local r.r in rxr[0]; all-reduce it in place
+    if (cg->dtype == CGX_F32) {
+      auto *st = (CgScalars<float> *)cg->st;
+      rc = peer_allreduce<float>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s);
+    } else {
+      auto *st = (CgScalars<double> *)cg->st;
+      rc = peer_allreduce<double>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s);
+    }
+    if (rc) return rc;
+  } else if (A->dist) {
     const size_t off = cg->dtype == CGX_F32 ? offsetof(CgScalars<float>, rxr)
                                             : offsetof(CgScalars<double>, rxr);
     if ((rc = dist_allreduce_scalar(cg->ctx, (char *)cg->st + off, cg->dtype, 1, s))) return rc;
@@ -1722,6 +1767,11 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   (void)hipEventDestroy(ev[0]);
   (void)hipEventDestroy(ev[1]);
   if (rc) return rc;
+  if (last_stopped == 3) {
+    set_error("peer transport: a device-side wait timed out (a rank stopped responding, or "
+              "$CGX_PEER_TIMEOUT_S is too short); the solve was stopped");
+    return CGX_ENCCL;
+  }
   if ((rc = flush_pending_x(cg))) return rc;
   CGX_HIP(hipStreamSynchronize(s));
   if (cg->timing) {

@@ -51,6 +51,45 @@ struct Halo {
   int64_t send_total = 0;
 };
 
+// Device peer transport over xGMI (cgx_peer.hip): the
+// iteration's halo exchange and both dot all-reduces as plain kernels that
+// store straight into the other ranks' memory (hipIpc-mapped, uncached), so
+// a partitioned iteration is all kernels and graph-capturable.
+constexpr int kPeerMax = 16;  // ranks of one node
+constexpr int kPushWG = 16;   // push workgroups (and flags) per neighbour
+struct PeerState {            // device, per matrix
+  unsigned long long ar;      // all-reduces completed (the tag of the last)
+  int fault;                  // a spin timed out: every later peer kernel returns
+  int pad;
+};
+struct PeerDev {  // kernel argument (by value)
+  char *ctl[kPeerMax];            // rank q's mailbox + flags, as mapped here
+  void *land_remote[kPeerMax];    // send neighbour i: where my values land on it
+  int send_rank[kPeerMax];        // send neighbour i's rank
+  int64_t send_off[kPeerMax];     // send neighbour i: first entry in send_idx
+  int64_t send_cnt[kPeerMax];
+  int recv_rank[kPeerMax];        // ranks whose values land here
+  const int *send_idx;
+  const void *land_local;         // my landing buffer (n_ghost values)
+  PeerState *state;
+  int64_t n_local, n_ghost;
+  long long spin_ticks;           // wall-clock ticks before a spin gives up
+  int rank, world, nsend, nrecv;
+};
+// mailbox layout inside a rank's ctl allocation: val[2][kPeerMax] doubles,
+// tag[2][kPeerMax] u64 (parity = tag & 1), then flag[kPeerMax][kPushWG] u64
+constexpr int kPeerTagOff = 2 * kPeerMax * 8;
+constexpr int kPeerFlagOff = 4 * kPeerMax * 8;
+constexpr size_t kPeerCtlBytes = kPeerFlagOff + (size_t)kPeerMax * kPushWG * 8;
+struct Peer {
+  bool on = false;
+  void *ctl = nullptr;    // this rank's ctl (uncached, IPC-exported)
+  void *land = nullptr;   // this rank's landing buffer (uncached, IPC-exported)
+  void *state = nullptr;  // PeerState
+  std::vector<void *> mapped;  // IPC mappings of other ranks' buffers
+  PeerDev dev{};
+};
+
 // Host-staged transport (cgx_dist_init_host): collectives are callbacks.
 struct HostComm {
   cgx_allgather_fn allgather;
@@ -106,6 +145,7 @@ struct cgx_csr {
   int *d_split = nullptr;
   int split_ni = 0, split_nb = 0;
   hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
+  cgx::Peer peer;  // device peer transport (cgx_dist_peer_enable)
   int64_t sell_padded = 0;
   int64_t sell_idx_words = 0;  // dictionary SELL index words
   int64_t vc_chunks = 0;       // value-code chunk-lanes (16 B each, 8 B in 4-bit form)
@@ -160,4 +200,15 @@ int dist_halo_post(cgx_csr *A, void *d_vec_ext, hipStream_t s, bool *async);
 int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipStream_t s);
 int dist_destroy_halo(cgx_csr *A);
 int dist_comm_destroy(cgx_ctx *ctx);
+// setup collective on host buffers over the setup transport (RCCL / host)
+int comm_allgather(cgx_ctx *ctx, const void *mine, size_t bytes, void *all);
+// cgx_peer.hip: the peer transport's per-iteration steps (enqueue on s)
+template <typename T> int peer_push(cgx_csr *A, const T *v_ext, CgScalars<T> *st, int slot,
+                                    hipStream_t s);
+template <typename T> int peer_wait(cgx_csr *A, T *v_ext, CgScalars<T> *st, int slot,
+                                    hipStream_t s);
+// *dst = sum over ranks of (sum of part[0..np)), identical bits on every rank
+template <typename T> int peer_allreduce(cgx_csr *A, const T *part, int np, T *dst,
+                                         CgScalars<T> *st, int slot, hipStream_t s);
+int peer_destroy(cgx_csr *A);
 }  // namespace cgx

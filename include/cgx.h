@@ -213,6 +213,19 @@ int cgx_csr_halo_info(cgx_csr *csr, int64_t *ghosts, int *neighbours);
  * when the matrix is not split (no SELL copy, or no ghosts). */
 int cgx_csr_split_info(cgx_csr *csr, int *interior_slices, int *boundary_slices);
 int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value);
+/* Device peer transport over xGMI for a partitioned matrix (collective):
+ * every rank maps the other ranks' mailboxes and its neighbours' halo
+ * landing buffers (hipIpc, uncached device memory), and the solver's halo
+ * exchange and dot all-reduces then run as kernels that store straight into
+ * peer memory — no host-enqueued collective per iteration, so the
+ * partitioned iteration is graph-captured like the single-GPU one. The
+ * transport is checked against the setup transport (RCCL or host) before it
+ * is used: *enabled = 1 when every rank passed, 0 when the solver keeps the
+ * setup transport (not an error; cgx_last_error() says why). Call before
+ * cgx_cg_create. $CGX_PEER=0 declines; $CGX_PEER_TIMEOUT_S bounds every
+ * device-side wait (default 10 s; a timeout stops the solve with an error). */
+int cgx_dist_peer_enable(cgx_csr *csr, int *enabled);
+int cgx_dist_peer_info(cgx_csr *csr, int *enabled);
 
 /* ---- host-only helpers (no device needed; the CPU test-suite drives them) --
  * Halo plan of rows [row_begin, row_begin + n_local) whose global column

@@ -16,6 +16,7 @@ line with the verdict.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import ctypes as C
 import json
 import os
@@ -41,7 +42,10 @@ def main():
                     help="fixed body count at tol 0, checked against the oracle's OpenMP "
                          "iteration (for large grids); -1: solve to --tol")
     ap.add_argument("--tol", type=float, default=1e-8)
-    ap.add_argument("--transport", choices=["rccl", "host"], default="rccl")
+    ap.add_argument("--transport", choices=["rccl", "host", "host-peer", "rccl-peer"],
+                    default="rccl",
+                    help="setup transport, and '-peer': the device peer transport for the "
+                         "iteration (cgx_dist_peer_enable; must pass its self-test)")
     ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,7 +55,7 @@ def main():
     L = lib()
     dev = local % max(1, cga.device_count())
     q = cga.Queue(dev)
-    if a.transport == "host":
+    if a.transport.startswith("host"):
         from conjugategradient_amd.hostcomm import HostTransport
         transport = HostTransport()
         transport.attach(q)
@@ -78,6 +82,12 @@ def main():
     A = C.c_void_p()
     check(L.cgx_csr_create_dist(q.handle, n, begin, nl, nnz, rows.ptr, cols.ptr, vals.ptr, F64,
                                 C.byref(A)))
+    peer = C.c_int(0)
+    if a.transport.endswith("-peer"):
+        check(L.cgx_dist_peer_enable(A, C.byref(peer)))
+        if not peer.value:
+            raise SystemExit(f"rank {rank}: peer transport unavailable: "
+                             f"{L.cgx_last_error().decode()}")
     ghosts, nbrs = C.c_int64(), C.c_int()
     check(L.cgx_csr_halo_info(A, C.byref(ghosts), C.byref(nbrs)))
     ni, nb = C.c_int(), C.c_int()
@@ -95,7 +105,8 @@ def main():
     acc = C.c_double()
     check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
     parts = [None] * world
-    dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value)))
+    dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value),
+                                   int(peer.value)))
     # x to rank 0 as tensors, padded to the largest block (gloo gathers
     # equal sizes; blocks differ by at most one row)
     mx = max(counts)
@@ -125,7 +136,9 @@ def main():
                           "oracle_bodies": oracle_bodies, "rel_err": relerr,
                           "accuracy": acc.value, "ghosts": [p[0] for p in parts],
                           "neighbours": [p[1] for p in parts],
-                          "split": [p[2] for p in parts], "ok": ok}), flush=True)
+                          "split": [p[2] for p in parts], "peer": [p[3] for p in parts],
+                          "x_sha": hashlib.sha256(xg.tobytes()).hexdigest()[:16],
+                          "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)
     L.cgx_csr_destroy(A)
     q.close()
