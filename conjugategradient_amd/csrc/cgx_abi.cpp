@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <tuple>
 #include <type_traits>
@@ -774,6 +775,8 @@ void free_sell(cgx_csr *A) {
   A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
+  A->dev.march_k = A->dev.march_a = A->dev.march_len = 0;
+  A->dev.march_pat = -1;
   A->sell_padded = 0;
   A->sell_idx_words = 0;
   A->vc_chunks = 0;
@@ -907,6 +910,42 @@ static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
   pool.resize(pool.size() + kSellPatMax, 0);  // the kernel reads up to 7 slots past a pattern
   voff_total = voff;
   return true;
+}
+
+// Plane-march plan (variant bit 2097152, cgx_kernels.hip spmv_sellpv_march):
+// the most common slice pattern must be {-D, -a, -1, 0, 1, a, D} (3-D
+// 7-point) or {-D, -1, 0, 1, D} (2-D 5-point) with D a positive multiple of
+// the 128-row slice and 1 < a < D. Slices with another pattern (or the same
+// pattern at another pool base) still run, through the per-slice form.
+// $CGX_MARCH=0 turns it off, $CGX_MARCH_LEN sets planes per run (A/B).
+static void plan_march(const std::vector<SellSlice> &sl, const std::vector<int> &pool,
+                       int64_t nx, size_t es, CsrDev &dev) {
+  dev.march_k = dev.march_a = dev.march_len = 0;
+  dev.march_pat = -1;
+  if (const char *e = std::getenv("CGX_MARCH"))
+    if (std::atoi(e) == 0) return;
+  if (sl.empty() || (uint64_t)nx * es >= (uint64_t(1) << 32)) return;
+  std::map<std::pair<int, int>, int64_t> freq;  // (pool base, width) -> slices
+  for (const SellSlice &m : sl) ++freq[{m.dict, m.width}];
+  auto best = freq.begin();
+  for (auto i = freq.begin(); i != freq.end(); ++i)
+    if (i->second > best->second) best = i;
+  const int base = best->first.first, W = best->first.second;
+  if (best->second * 2 < (int64_t)sl.size() || (W != 5 && W != 7)) return;
+  const int *o = pool.data() + base;
+  const int D = o[W - 1], H = 2 * kSellRows;
+  if (D <= 0 || D % H != 0 || o[0] != -D) return;
+  int a = 0;
+  if (W == 7) {
+    a = o[5];
+    if (!(a > 1 && a < D && o[1] == -a && o[2] == -1 && o[3] == 0 && o[4] == 1)) return;
+  } else if (!(o[1] == -1 && o[2] == 0 && o[3] == 1)) {
+    return;
+  }
+  dev.march_k = D / H;
+  dev.march_a = a;
+  dev.march_pat = base;
+  if (const char *e = std::getenv("CGX_MARCH_LEN")) dev.march_len = std::max(0, std::atoi(e));
 }
 
 extern "C" int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
@@ -1222,6 +1261,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   A->dev.nx = nx;
   A->dev.sell_maxw = 0;
   for (const SellSlice &m : sl) A->dev.sell_maxw = std::max(A->dev.sell_maxw, m.width);
+  if (kind == 1) plan_march(sl, pool, nx, dtype_size(A->dtype), A->dev);
   A->sell_padded = voff;
   A->sell_idx_words = (int64_t)idx.size();
   if (kind && A->dtype == CGX_F32)
@@ -1285,6 +1325,15 @@ extern "C" int cgx_csr_value_codes(cgx_csr *A, int *n_values) {
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_march_info(cgx_csr *A, int *stride, int *offset_a, int *run_planes) {
+  CGX_REQUIRE(A && stride && offset_a && run_planes, CGX_EINVAL, "NULL argument");
+  const bool on = A->dev.svc && A->dev.sell_maxw <= 8 && A->dev.march_k > 0;
+  *stride = on ? A->dev.march_k : 0;
+  *offset_a = on ? A->dev.march_a : 0;
+  *run_planes = on ? A->dev.march_len : 0;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
   if (has_sell) *has_sell = !A->dev.sl ? 0 : (A->dev.sell_kind ? 3 : A->dev.sell_r);
@@ -1302,7 +1351,8 @@ static bool known_variant(int v) {
     if (k == v) return true;
   // the resolved SELL-P forms cgx_csr_variant reports (e.g. 1875970) are
   // accepted back as requests
-  constexpr int sellp_bits = 8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2;
+  constexpr int sellp_bits =
+      8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2097152 | 2;
   return (v & 8192) && !(v & ~sellp_bits);
 }
 
@@ -1364,8 +1414,9 @@ int autotune_spmv(cgx_csr *A) {
   // 1048576: one gather pair fewer per offset -1 / +1)
   for (int c4 : {0, 262144}) {
     if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
-    for (int pipe : {0, 524288, 524288 | 1048576}) {
+    for (int pipe : {0, 524288, 524288 | 1048576, 524288 | 1048576 | 2097152}) {
       if (pipe && A->dev.sell_maxw > 8) continue;
+      if ((pipe & 2097152) && A->dev.march_k < 1) continue;
       if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
       cands.push_back(2050 | 32768 | c4 | pipe);
     }

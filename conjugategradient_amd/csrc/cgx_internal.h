@@ -133,6 +133,10 @@ struct CsrDev {
   // 4-bit codes (variant bit 262144; at most kVc4Max values): 8 bytes per
   // lane per chunk, byte j = slot j, row 0 in the low nibble
   const void *svc4 = nullptr;
+  // plane march (variant bit 2097152; cgx_abi.cpp plan_march): the dominant
+  // SELL-P pattern is {-D, (-a,) -1, 0, 1, (a,) D} with D = 128 march_k rows
+  // at pool base march_pat; march_len: planes per run (0: fill the grid)
+  int march_k = 0, march_a = 0, march_pat = -1, march_len = 0;
 };
 
 template <typename T> struct Launch {

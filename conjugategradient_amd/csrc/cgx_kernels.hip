@@ -257,6 +257,10 @@ struct CsrArgs {
   const void *svc;    // SELL-P value codes (variant bit 32768)
   const void *svdict; // their dictionary (kVcDict entries)
   const void *svc4;   // 4-bit value codes (variant bit 262144)
+  // plane march (variant bit 2097152): slices a plane apart (0: no march
+  // pattern), the pattern's +-a offset (0: 2-D form), its pool base, and
+  // the run length in planes (0: fill the grid)
+  int mk, mo, mpat, ml;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -1558,12 +1562,219 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
   }
 }
 
+// Plane march (variant bit 2097152, on the pipelined stencil form 1875968):
+// for a matrix whose dominant slice pattern is {-D, -a, -1, 0, +1, +a, +D}
+// (3-D 7-point: a = nx, D = nx ny) or {-D, -1, 0, +1, +D} (2-D 5-point:
+// D = nx) with D a multiple of the 128-row slice (D = 128 K), a wave walks
+// the slices c, c + K, c + 2K, ... of one column through a run of L planes
+// instead of consecutive slices. The x pairs at -D and +D of slice s are the
+// center pairs of the slices before and after it in the walk, already in
+// registers: no gathers. In the consecutive walk each x line is fetched as
+// the center, and again as the +D and -D gathers of slices a plane away,
+// after 1-3 MB of other traffic passed the XCD's L2. Here it is fetched
+// once as a center (plus one extra center per end of a run), so only the
+// +-a gathers (the same plane, neighbouring columns walked in step by the
+// neighbouring waves) go to L2. Per slice: code word, center pair of
+// s + 2K, +-a gathers, one edge load (lane 0: x[first - 1], lane 63:
+// x[first + 128], the DPP shifts' fill values), the Ap store; the loads of
+// slice s + K are issued before slice s sums. The per-row sums run in the
+// same slot order as every SELL-P form, so Ap is bit-identical.
+// Slices that are not of the march pattern (boundary planes and lines, the
+// ragged end) run sellpv_slice2. Work items are (run z, column c), z-major,
+// split over the XCDs like slices (sell_range); L from A.ml or, when 0, so
+// that the items about fill the grid's waves. Needs every slice <= 8 wide
+// (one code chunk per slice: slice s's codes at chunk s).
+template <typename T, int V, bool S3, class Epi, class Gather>
+__device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather &x, Epi &epi,
+                                                  const T *__restrict__ vd) {
+  constexpr bool NT = (V & 2) != 0;
+  constexpr bool C4 = (V & 262144) != 0;
+  constexpr int H = 2 * kSellRows;
+  using PV = typename PairU<T>::V;
+  const Ull2 *__restrict__ codes = static_cast<const Ull2 *>(A.svc);
+  const unsigned long long *__restrict__ codes4 =
+      static_cast<const unsigned long long *>(A.svc4);
+  const int lane = threadIdx.x & 63;
+  const int K = A.mk, nsl = (int)A.nsl;
+  const int nfull = (int)(A.n / H);  // slices whose 128 rows all exist
+  const int a = A.mo;  // the +-a slots of the 3-D form
+  constexpr int W7 = S3 ? 7 : 5;
+  const int nxm2 = (int)A.nx - 2;
+  const int planes = (nsl + K - 1) / K;
+  int L = A.ml;
+  if (L <= 0) {
+    const int zc = max(1, (int)gridDim.x * (kBlock / 64) / K);
+    L = (planes + zc - 1) / zc;
+  }
+  const int Z = (planes + L - 1) / L;
+  // byte offsets into x fit 32 bits (else every slice takes sellpv_slice2)
+  const bool off32 = (uint64_t)A.nx * sizeof(T) < (uint64_t(1) << 32);
+  int it, step, end, lo;
+  sell_range(K * Z, it, step, end, lo);
+  auto code_at = [&](int sl) {
+    Ull2 cw;
+    if constexpr (C4) {
+      cw.x = ldg<NT>(codes4 + (int64_t)sl * kSellRows + lane);
+      cw.y = 0;
+    } else {
+      cw = ldg<NT>(codes + (int64_t)sl * kSellRows + lane);
+    }
+    return cw;
+  };
+  auto center = [&](int sl) { return x.pair(min(sl * H + 2 * lane, nxm2)); };
+  // slice descriptors (dict, width) by VECTOR loads: a scalar load in the
+  // loop would make every LDS dictionary read wait for it (SMEM returns out
+  // of order, so any LDS use waits lgkmcnt(0)); `zv` is an opaque zero that
+  // keeps the address divergent to the compiler
+  int zv;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
+  const Int2 *__restrict__ cdw = reinterpret_cast<const Int2 *>(
+      reinterpret_cast<const char *>(A.sl) + offsetof(SellSlice, dict));
+  auto desc = [&](int sl) { return cdw[(int64_t)sl * (sizeof(SellSlice) / sizeof(Int2)) + zv]; };
+  auto uni = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+  // slice sl walks the march pattern: its descriptor names the pattern, its
+  // +-D neighbours exist (whole slices of rows), every pair lies inside x
+  auto fast = [&](int sl, int dict, int w) {
+    return off32 && dict == A.mpat && w == W7 && sl >= K && sl + K < nfull;
+  };
+  for (; it < end; it += step) {
+    const int z = it / K, c = it - z * K;
+    int s = c + z * L * K;
+    if (s >= nsl) continue;
+    const int last = min(c + ((z + 1) * L - 1) * K, c + (nsl - 1 - c) / K * K);
+    // every load is issued, at safe addresses for a slice that is not fast
+    // (a fixed load count keeps the compiler's in-order vmcnt waits exact)
+    struct Batch {
+      Ull2 cw;
+      PV gm, gp;
+      T edge;
+    };
+    auto issue = [&](int sl, bool fs, Batch &b) {
+      b.cw = code_at(sl);
+      const int fr = sl * H;
+      const unsigned rb = (unsigned)min(fr + 2 * lane, nxm2) * (unsigned)sizeof(T);
+      if constexpr (S3) {
+        // bit 16 (timing ablation, spmv_dot only): the +-a gathers re-read
+        // the slice's own center
+        const unsigned ab =
+            fs && !(V & 16) ? (unsigned)a * (unsigned)sizeof(T) : 0u;
+        b.gm = x.pair_b(rb - ab);
+        b.gp = x.pair_b(rb + ab);
+      }
+      b.edge = x(fs ? (lane == 63 ? fr + H : fr - 1) : fr);
+    };
+    // slice s from its batch and the center pairs of s - K, s, s + K
+    auto sum = [&](int s, bool f, const Batch &b, const PV &cprev, const PV &ccur,
+                   const PV &cnext) {
+      if (f) {
+        const int r0 = s * H + 2 * lane;
+        T g0[8], g1[8];
+        const T left = wave_shr1(ccur.y, b.edge), right = wave_shl1(ccur.x, b.edge);
+        constexpr int K1 = S3 ? 2 : 1;  // slot of offset -1
+        g0[0] = cprev.x;
+        g1[0] = cprev.y;
+        if constexpr (S3) {
+          g0[1] = b.gm.x;
+          g1[1] = b.gm.y;
+          g0[5] = b.gp.x;
+          g1[5] = b.gp.y;
+        }
+        g0[K1] = left;
+        g1[K1] = ccur.x;
+        g0[K1 + 1] = ccur.x;
+        g1[K1 + 1] = ccur.y;
+        g0[K1 + 2] = ccur.y;
+        g1[K1 + 2] = right;
+        g0[W7 - 1] = cnext.x;
+        g1[W7 - 1] = cnext.y;
+        epi.pre2c(r0, r0 + 1, ccur.x, ccur.y);
+        T acc0 = T(0), acc1 = T(0);
+#pragma unroll
+        for (int j = 0; j < W7; ++j) {
+          unsigned k0, k1;
+          bool on0, on1;
+          if constexpr (C4) {
+            k0 = (unsigned)(b.cw.x >> (8 * j)) & 0xfu;
+            k1 = (unsigned)(b.cw.x >> (8 * j + 4)) & 0xfu;
+            on0 = k0 != 0xfu;
+            on1 = k1 != 0xfu;
+          } else {
+            const unsigned long long w = j < 4 ? b.cw.x : b.cw.y;
+            k0 = (unsigned)(w >> (16 * (j & 3))) & 0xffu;
+            k1 = (unsigned)(w >> (16 * (j & 3) + 8)) & 0xffu;
+            on0 = k0 != kVcAbsent;
+            on1 = k1 != kVcAbsent;
+          }
+          const T t0 = acc0 + vd[k0] * g0[j];
+          const T t1 = acc1 + vd[k1] * g1[j];
+          acc0 = on0 ? t0 : acc0;
+          acc1 = on1 ? t1 : acc1;
+        }
+        epi.row2(r0, acc0, acc1, true, true);
+      } else {
+        sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd, s);
+        // drain: this path's load count is not fixed (a loop over code
+        // chunks); a merge with an unknown count would make the compiler
+        // wait vmcnt(0) before the next descriptor on every step
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
+      }
+    };
+    // one step: the next slice's descriptor decides its batch; issue that
+    // batch, the descriptor after it and the center two planes on; then sum
+    // slice s (whose loads were issued one step earlier). Buffers rotate by
+    // argument, never by copy: a copy of a register whose load is in flight
+    // waits for it (the loop below is unrolled four times so every role
+    // returns to its register).
+    auto stepf = [&](int &s, bool &f, const Int2 &dcur, Int2 &dnew, const Batch &bc, Batch &bn,
+                     const PV &cm, const PV &c0, const PV &cp, PV &cnn) {
+      const int sn = s + K;
+      const bool has_next = sn <= last;
+      const bool fn = has_next && fast(sn, uni(dcur.x), uni(dcur.y));
+      __builtin_amdgcn_sched_barrier(0);
+      const int snk = has_next ? sn : s;
+      const int snn = min(snk + K, nsl - 1);
+      dnew = desc(snn);
+      issue(snk, fn, bn);
+      cnn = center(snn);
+      __builtin_amdgcn_sched_barrier(0);
+      sum(s, f, bc, cm, c0, cp);
+      s = sn;
+      f = fn;
+      return has_next;
+    };
+    // prologue: slice s's batch, the centers of s - K, s, s + K, the
+    // descriptor of s + K
+    // descriptor of s + K (the first step's) early: the first step waits
+    // for it, and so for every load issued before it
+    const Int2 d0 = desc(s);
+    Int2 dA = desc(min(s + K, nsl - 1)), dB;
+    PV c0 = center(max(s - K, 0)), c1 = center(s), c2, c3;
+    bool f = fast(s, uni(d0.x), uni(d0.y));
+    Batch bA, bB;
+    issue(s, f, bA);
+    c2 = center(min(s + K, nsl - 1));
+    for (;;) {
+      if (!stepf(s, f, dA, dB, bA, bB, c0, c1, c2, c3)) break;
+      if (!stepf(s, f, dB, dA, bB, bA, c1, c2, c3, c0)) break;
+      if (!stepf(s, f, dA, dB, bA, bB, c2, c3, c0, c1)) break;
+      if (!stepf(s, f, dB, dA, bB, bA, c3, c0, c1, c2)) break;
+    }
+  }
+}
+
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, Epi &epi,
                                             T *vd) {
   const T *__restrict__ src = static_cast<const T *>(A.svdict);
   for (int i = threadIdx.x; i < kVcDict; i += kBlock) vd[i] = src[i];
   __syncthreads();
+  if constexpr ((V & 2097152) != 0) {
+    if (A.mk > 0) {
+      if (A.mo > 0) spmv_sellpv_march<T, V, true, Epi, Gather>(A, x, epi, vd);
+      else spmv_sellpv_march<T, V, false, Epi, Gather>(A, x, epi, vd);
+      return;
+    }
+  }
   if constexpr ((V & 524288) != 0) {
     spmv_sellpv_pipe<T, V, Epi, Gather>(A, x, epi, vd);
     return;
@@ -2280,7 +2491,8 @@ inline int elem_grid(int64_t n, int per_thread) {
 inline CsrArgs args(const CsrDev &A) {
   return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
                  A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
-                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4};
+                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4,
+                 A.march_k, A.march_a, A.march_pat, A.march_len};
 }
 
 }  // namespace
@@ -2506,7 +2718,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     if (A.sl && A.sell_kind && (v & 32768) && A.svc)
       return 32768 | 8192 |
              (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
-                   (A.sell_maxw <= 8 ? 524288 | 1048576 : 0)));
+                   (A.sell_maxw <= 8 ? 524288 | 1048576 : 0) |
+                   (A.sell_maxw <= 8 && A.march_k > 0 ? 2097152 : 0)));
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2596,6 +2809,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 1613826: CGX_LAUNCH_V(KERNEL, 1613826, __VA_ARGS__);                         \
     case 1875968: CGX_LAUNCH_V(KERNEL, 1875968, __VA_ARGS__);                         \
     case 1875970: CGX_LAUNCH_V(KERNEL, 1875970, __VA_ARGS__);                         \
+    case 3710976: CGX_LAUNCH_V(KERNEL, 3710976, __VA_ARGS__);                         \
+    case 3710978: CGX_LAUNCH_V(KERNEL, 3710978, __VA_ARGS__);                         \
+    case 3973120: CGX_LAUNCH_V(KERNEL, 3973120, __VA_ARGS__);                         \
+    case 3973122: CGX_LAUNCH_V(KERNEL, 3973122, __VA_ARGS__);                         \
     default: return hipErrorInvalidValue;                                      \
   }
 
@@ -2611,7 +2828,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(267) X(140) X(141) X(142) X(143) X(76) X(77) X(78) X(79) X(2048) X(2050) X(2056)  \
   X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)        \
   X(40978) X(106498) X(172034) X(303104) X(303106) X(303122) X(827392) X(827394)        \
-  X(827410) X(565248) X(565250) X(1613824) X(1613826) X(1875968) X(1875970)
+  X(827410) X(565248) X(565250) X(1613824) X(1613826) X(1875968) X(1875970) \
+  X(3710976) X(3710978) X(3973120) X(3973122)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \
@@ -2679,7 +2897,7 @@ template <typename T>
 hipError_t Launch<T>::spmv_dot_slices(const CsrDev &A, const int *list, int count, int part_off,
                                       const T *p, T *Ap, CgScalars<T> *st, int slot,
                                       RedWs<T> *ws, hipStream_t s, int rev) {
-  const int v = spmv_variant<T>(A);
+  const int v = spmv_variant<T>(A) & ~2097152;  // a slice list is walked in list order
   if (!(v & (2048 | 8192)) || count < 1) return hipErrorInvalidValue;
   CsrArgs a = args(A);
   a.sorder = list;
@@ -2691,7 +2909,8 @@ hipError_t Launch<T>::spmv_dot_slices(const CsrDev &A, const int *list, int coun
 }
 template <typename T> int Launch<T>::slice_grid(const CsrDev &A, int count) {
   const int g = (count + 3) / 4;  // one wave per slice, 4 waves per workgroup
-  return cap_resident<T>(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g), spmv_variant<T>(A));
+  return cap_resident<T>(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g),
+                         spmv_variant<T>(A) & ~2097152);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
@@ -2714,6 +2933,7 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 172034: CGX_LAUNCH_V(k_spmv_dot, 172034, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 303122: CGX_LAUNCH_V(k_spmv_dot, 303122, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 827410: CGX_LAUNCH_V(k_spmv_dot, 827410, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 3973138: CGX_LAUNCH_V(k_spmv_dot, 3973138, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);

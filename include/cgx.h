@@ -99,6 +99,13 @@ int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
  * cgx_csr_create when the SELL-P copy exists and the matrix has that few
  * distinct values; $CGX_VALUE_CODES=0 disables it), 0 when it has none. */
 int cgx_csr_value_codes(cgx_csr *csr, int *n_values);
+/* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
+ * *stride = slices (of 128 rows) between a slice and its +-D neighbour
+ * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D
+ * a multiple of 128 rows, and the bit is ignored), *offset_a = the 3-D
+ * form's +-a offset (0: 2-D form), *run_planes = planes per run (0: chosen
+ * per launch to fill the grid; $CGX_MARCH_LEN sets it). */
+int cgx_csr_march_info(cgx_csr *csr, int *stride, int *offset_a, int *run_planes);
 /* Bytes of the matrix stream one SpMV launch in the matrix's current
  * variant reads (values, indices / codes / masks, slice descriptors;
  * vectors excluded): the format's algorithmic bytes, next to CSR's
