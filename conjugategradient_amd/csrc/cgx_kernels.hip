@@ -1432,7 +1432,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = pat[pb + min(j, W - 1)];
   }
-  Ull2 cw = code_at(cs[si].ioff);
+  Ull2 cwA = code_at(cs[si].ioff), cwB;
   // slice si is interior when the pairs of its lowest and highest offset
   // (o[0], o[7] = o[W-1]: the pattern is sorted) lie inside x for every
   // lane, dead lanes of a last partial slice included, and byte offsets
@@ -1442,7 +1442,11 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     const int fr = sl * (2 * kSellRows);
     return off32 && fr + omin >= 0 && fr + 2 * kSellRows - 2 + omax <= nxm2;
   };
-  for (;;) {
+  // one slice; the code word rotates by argument, never by copy (a copy of
+  // a register whose load is in flight waits for it, and at the loop's
+  // back edge that wait also drained the Ap store: the prefetch never
+  // overlapped anything). The loop below runs it twice per trip.
+  auto body = [&](const Ull2 &cw, Ull2 &cwn) -> bool {
     const int ns = s + step;
     const bool has_next = ns < end;
     const int nk = has_next ? ns : s;
@@ -1527,7 +1531,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     int on[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) on[j] = pat[pbn + min(j, Wn - 1)];
-    const Ull2 cwn = code_at(coffn);
+    cwn = code_at(coffn);
     __builtin_amdgcn_sched_barrier(0);
     T acc0 = T(0), acc1 = T(0);
 #pragma unroll
@@ -1552,13 +1556,15 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
       acc1 = on1 ? t1 : acc1;
     }
     epi.row2(r0, acc0, acc1, l0, l1);
-    if (!has_next) break;
+    if (!has_next) return false;
     si = sn;
     W = Wn;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = on[j];
-    cw = cwn;
     s = ns;
+    return true;
+  };
+  while (body(cwA, cwB) && body(cwB, cwA)) {
   }
 }
 
