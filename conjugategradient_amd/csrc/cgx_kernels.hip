@@ -1659,11 +1659,11 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
       b.cw = code_at(sl);
       const int fr = sl * H;
       const unsigned rb = (unsigned)min(fr + 2 * lane, nxm2) * (unsigned)sizeof(T);
-      if constexpr (S3) {
-        // bit 16 (timing ablation, spmv_dot only): the +-a gathers re-read
-        // the slice's own center
-        const unsigned ab =
-            fs && !(V & 16) ? (unsigned)a * (unsigned)sizeof(T) : 0u;
+      if constexpr (S3 && (V & 16) != 0) {
+        // bit 16 (timing ablation, spmv_dot only): no +-a gathers at all
+        b.gm.x = b.gm.y = b.gp.x = b.gp.y = T(rb & 1);
+      } else if constexpr (S3) {
+        const unsigned ab = fs ? (unsigned)a * (unsigned)sizeof(T) : 0u;
         b.gm = x.pair_b(rb - ab);
         b.gp = x.pair_b(rb + ab);
       }
