@@ -93,6 +93,8 @@ _SIGS = {
     "cgx_dist_init": (_i32, [_vp, _i32, _i32, C.c_char_p, _sz]),
     "cgx_dist_init_host": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp]),
     "cgx_dist_rank": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
+    "cgx_dist_host_async": (_i32, [_vp, _i32]),
+    "cgx_csr_halo_async_calls": (_i32, [_vp, C.POINTER(_i64)]),
     "cgx_csr_create_dist": (_i32, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i32,
                                    C.POINTER(_vp)]),
     "cgx_csr_halo_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i32)]),

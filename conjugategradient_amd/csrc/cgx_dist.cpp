@@ -170,13 +170,49 @@ int dist_halo_exchange(cgx_csr *A, void *vec_ext, hipStream_t s) {
   return CGX_OK;
 }
 
+// The asynchronous host transport's exchange: a host function on the comm
+// stream, between the D2H of the packed entries and the H2D of the ghosts. It
+// runs on the runtime's callback thread and makes no HIP calls; a failure is
+// kept in async_rc and reported by the next host collective (which
+// synchronises the solver stream, itself behind ev_halo).
+static void host_exchange_cb(void *arg) {
+  auto *A = (cgx_csr *)arg;
+  Halo &h = A->halo;
+  const size_t es = dtype_size(A->dtype);
+  char *hs = (char *)h.h_send, *hr = (char *)h.h_recv;
+  std::vector<const void *> sp;
+  std::vector<void *> rp;
+  std::vector<size_t> sb, rb;
+  for (size_t i = 0; i < h.nbr.size(); ++i) {
+    sp.push_back(hs + (size_t)h.send_off[i] * es);
+    sb.push_back((size_t)h.send_cnt[i] * es);
+    rp.push_back(hr + (size_t)h.recv_off[i] * es);
+    rb.push_back((size_t)h.recv_cnt[i] * es);
+  }
+  const int r = A->ctx->host->exchange(A->ctx->host->user, (int)h.nbr.size(), h.nbr.data(),
+                                       sp.data(), sb.data(), rp.data(), rb.data());
+  if (r != 0) A->ctx->host_async_rc.store(r);
+}
+
+static int dist_async_status(cgx_ctx *ctx) {
+  const int r = ctx->host_async_rc.exchange(0);
+  if (r) {
+    set_error("asynchronous host halo exchange callback failed (%d)", r);
+    return CGX_ENCCL;
+  }
+  return CGX_OK;
+}
+
 int dist_halo_post(cgx_csr *A, void *vec_ext, hipStream_t s, bool *async) {
   *async = false;
   cgx_ctx *ctx = A->ctx;
   Halo &h = A->halo;
   if (!A->dist || !multi(ctx) || (h.n_ghost == 0 && h.send_total == 0)) return CGX_OK;
-  if (ctx->host || !ctx->cstream || !A->ev_pack || !A->ev_halo)
+  const bool host_async = ctx->host && ctx->host_async;
+  if ((ctx->host && !host_async) || !ctx->cstream || !A->ev_pack || !A->ev_halo)
     return dist_halo_exchange(A, vec_ext, s);  // synchronous
+  int rc;
+  if ((rc = dist_async_status(ctx))) return rc;
   const size_t es = dtype_size(A->dtype);
   if (h.send_total > 0) {
     if (A->dtype == CGX_F32)
@@ -190,6 +226,20 @@ int dist_halo_post(cgx_csr *A, void *vec_ext, hipStream_t s, bool *async) {
   // it on s) is done; the interior rows proceed on s meanwhile
   CGX_HIP(hipEventRecord(A->ev_pack, s));
   CGX_HIP(hipStreamWaitEvent(ctx->cstream, A->ev_pack, 0));
+  if (host_async) {
+    // D2H, the exchange as a host function, H2D — all ordered on cstream
+    if (h.send_total)
+      CGX_HIP(hipMemcpyAsync(h.h_send, h.d_send_buf, (size_t)h.send_total * es,
+                             hipMemcpyDeviceToHost, ctx->cstream));
+    CGX_HIP(hipLaunchHostFunc(ctx->cstream, host_exchange_cb, A));
+    if (h.n_ghost)
+      CGX_HIP(hipMemcpyAsync((char *)vec_ext + (size_t)A->dev.n * es, h.h_recv,
+                             (size_t)h.n_ghost * es, hipMemcpyHostToDevice, ctx->cstream));
+    CGX_HIP(hipEventRecord(A->ev_halo, ctx->cstream));
+    h.async_calls += 1;
+    *async = true;
+    return CGX_OK;
+  }
   const ncclDataType_t t = nccl_type(A->dtype);
   CGX_NCCL(ncclGroupStart());
   for (size_t i = 0; i < h.nbr.size(); ++i) {
@@ -214,6 +264,8 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
     auto *h = (char *)ctx->h_pinned + 512;  // [0, 512) is cgx_cg_run's poll staging
     CGX_HIP(hipMemcpyAsync(h, d_val, es * count, hipMemcpyDeviceToHost, s));
     CGX_HIP(hipStreamSynchronize(s));
+    int rc;
+    if ((rc = dist_async_status(ctx))) return rc;  // a failed exchange: stop before the collective
     double v[8];
     for (int i = 0; i < count; ++i)
       v[i] = dtype == CGX_F32 ? (double)((float *)h)[i] : ((double *)h)[i];
@@ -224,7 +276,7 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
     }
     CGX_HIP(hipMemcpyAsync(d_val, h, es * count, hipMemcpyHostToDevice, s));
     CGX_HIP(hipStreamSynchronize(s));
-    return CGX_OK;
+    return dist_async_status(ctx);  // s waited on every halo posted before
   }
   CGX_NCCL(ncclAllReduce(d_val, d_val, (size_t)count, nccl_type(dtype), ncclSum, ctx->comm, s));
   return CGX_OK;
@@ -369,6 +421,27 @@ extern "C" int cgx_dist_init_host(cgx_ctx *ctx, int rank, int world, cgx_allgath
   ctx->host = new HostComm{ag, ar, ex, user};
   ctx->rank = rank;
   ctx->world = world;
+  return CGX_OK;
+}
+
+// Host transport only: run the per-iteration halo exchange on a comm stream
+// (D2H, the exchange callback as a host function, H2D, then an event the
+// solver stream waits on) so that a split SpMV's interior slices overlap it —
+// the same stream/event ordering as the RCCL exchange. Call before creating
+// the partitioned matrices (their events are made at creation).
+extern "C" int cgx_dist_host_async(cgx_ctx *ctx, int on) {
+  CGX_REQUIRE(ctx, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(ctx->host, CGX_ESTATE, "no host transport (cgx_dist_init_host first)");
+  CGX_HIP(hipSetDevice(ctx->device));
+  if (on && !ctx->cstream && ctx->world > 1)
+    CGX_HIP(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+  ctx->host_async = on != 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_halo_async_calls(cgx_csr *A, int64_t *calls) {
+  CGX_REQUIRE(A && calls, CGX_EINVAL, "NULL argument");
+  *calls = A->halo.async_calls;
   return CGX_OK;
 }
 

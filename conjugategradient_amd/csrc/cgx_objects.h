@@ -49,6 +49,7 @@ struct Halo {
   void *h_send = nullptr;          // pinned staging (host transport only)
   void *h_recv = nullptr;
   int64_t send_total = 0;
+  int64_t async_calls = 0;         // exchanges posted on the comm stream (host transport)
 };
 
 // Device peer transport over xGMI (cgx_peer.hip): the
@@ -118,7 +119,11 @@ struct cgx_ctx {
   ncclComm *comm = nullptr;
   cgx::HostComm *host = nullptr;
   int rank = 0, world = 1;
-  hipStream_t cstream = nullptr;  // RCCL halo exchange, overlapped with interior rows
+  hipStream_t cstream = nullptr;  // halo exchange, overlapped with interior rows
+  bool host_async = false;        // host transport: exchange on cstream (cgx_dist_host_async)
+  // the asynchronous exchange callback's status (a host function on cstream;
+  // read once the solver stream, which waited on it, has synchronised)
+  std::atomic<int> host_async_rc{0};
 };
 
 struct cgx_csr {

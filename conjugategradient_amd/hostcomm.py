@@ -84,8 +84,15 @@ class HostTransport:
 
         self._cbs = (AG(allgather), AR(allreduce), EX(exchange))
 
-    def attach(self, queue) -> None:
+    def attach(self, queue, overlap: bool = False) -> None:
+        """overlap: run the halo exchange on libcgx's comm stream
+        (cgx_dist_host_async): the exchange callback then runs on the HIP
+        runtime's callback thread while the interior slices compute. Only one
+        thread of a rank issues collectives at a time: the solver stream
+        waits for the exchange before the next all-reduce is staged."""
         check(lib().cgx_dist_init_host(queue.handle, self.rank, self.world,
                                        C.cast(self._cbs[0], C.c_void_p),
                                        C.cast(self._cbs[1], C.c_void_p),
                                        C.cast(self._cbs[2], C.c_void_p), None))
+        if overlap:
+            check(lib().cgx_dist_host_async(queue.handle, 1))

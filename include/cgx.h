@@ -205,6 +205,14 @@ typedef int (*cgx_exchange_fn)(void *user, int n, const int *peers, const void *
                                const size_t *recv_bytes);
 int cgx_dist_init_host(cgx_ctx *ctx, int rank, int world, cgx_allgather_fn allgather,
                        cgx_allreduce_fn allreduce, cgx_exchange_fn exchange, void *user);
+/* Host transport, asynchronous halo: the per-iteration exchange runs on the
+ * context's comm stream (D2H, `exchange` as a host function, H2D, an event the
+ * solver stream waits on), so a split SpMV's interior slices overlap it — the
+ * stream/event ordering of the RCCL exchange. The callback then runs on the
+ * HIP runtime's callback thread. Call before cgx_csr_create_dist. */
+int cgx_dist_host_async(cgx_ctx *ctx, int on);
+/* exchanges a partitioned matrix has posted on the comm stream (host transport) */
+int cgx_csr_halo_async_calls(cgx_csr *A, int64_t *calls);
 /* Local block of a globally row-partitioned matrix: rows
  * [row_begin, row_begin + n_local) with GLOBAL column indices (device arrays,
  * caller-owned, d_col is rewritten in place to local/ghost numbering).

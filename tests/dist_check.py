@@ -42,10 +42,12 @@ def main():
                     help="fixed body count at tol 0, checked against the oracle's OpenMP "
                          "iteration (for large grids); -1: solve to --tol")
     ap.add_argument("--tol", type=float, default=1e-8)
-    ap.add_argument("--transport", choices=["rccl", "host", "host-peer", "rccl-peer"],
+    ap.add_argument("--transport", choices=["rccl", "host", "host-async", "host-peer", "rccl-peer"],
                     default="rccl",
                     help="setup transport, and '-peer': the device peer transport for the "
-                         "iteration (cgx_dist_peer_enable; must pass its self-test)")
+                         "iteration (cgx_dist_peer_enable; must pass its self-test); "
+                         "'host-async': the host exchange on the comm stream, overlapped "
+                         "with the interior slices (cgx_dist_host_async)")
     ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -58,7 +60,7 @@ def main():
     if a.transport.startswith("host"):
         from conjugategradient_amd.hostcomm import HostTransport
         transport = HostTransport()
-        transport.attach(q)
+        transport.attach(q, overlap=a.transport == "host-async")
     else:
         uid = C.create_string_buffer(128)
         if rank == 0:
@@ -102,11 +104,13 @@ def main():
     bodies, rxr = C.c_int64(), C.c_double()
     tol = 0.0 if a.bodies >= 0 else a.tol
     check(L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, a.bodies, C.byref(bodies), C.byref(rxr)))
+    acalls = C.c_int64()
+    check(L.cgx_csr_halo_async_calls(A, C.byref(acalls)))
     acc = C.c_double()
     check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
     parts = [None] * world
     dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value),
-                                   int(peer.value)))
+                                   int(peer.value), int(acalls.value)))
     # x to rank 0 as tensors, padded to the largest block (gloo gathers
     # equal sizes; blocks differ by at most one row)
     mx = max(counts)
@@ -137,6 +141,7 @@ def main():
                           "accuracy": acc.value, "ghosts": [p[0] for p in parts],
                           "neighbours": [p[1] for p in parts],
                           "split": [p[2] for p in parts], "peer": [p[3] for p in parts],
+                          "async_exchanges": [p[4] for p in parts],
                           "x_sha": hashlib.sha256(xg.tobytes()).hexdigest()[:16],
                           "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)
