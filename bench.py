@@ -73,8 +73,17 @@ def update_bytes_per_iter(n: int, mode: int) -> int:
     (24 n) in three bodies of four and in the fourth also applies
     x += a0 p0 + .. + a3 p3 (reads x and the three other p buffers, writes x:
     +40 n), 34 n on average."""
+    if mode == 4:  # the p update is folded into the SpMV (spmv_bytes_per_iter);
+        return 24 * n + 12 * n  # the slot-3 x flush: x r/w + 4 p reads, once per 4 bodies
     xp = 40 * n if mode == 1 else 34 * n
     return 24 * n + xp
+
+
+def spmv_bytes_per_iter(stream_bytes: int, n: int, mode: int) -> int:
+    """The SpMV launch: its matrix stream (cgx_csr_stream_bytes) + p read + Ap
+    written (16 n); mode 4's k_spmv_fd reads r and p_{k-1} and writes p_k and
+    Ap (32 n)."""
+    return stream_bytes + (32 * n if mode == 4 else 16 * n)
 
 
 def parse(argv=None):
@@ -99,9 +108,10 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
-    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3], default=0,
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
-                         "2 fused (single GPU), 3 three kernels with the x update deferred")
+                         "2 fused (single GPU), 3 three kernels with the x update deferred, "
+                         "4 two kernels (p update folded into the SpMV), x deferred")
     ap.add_argument("--transport", choices=["auto", "rccl", "peer", "host", "host-peer"],
                     default="auto",
                     help="N>1 collectives: auto (device peer transport over xGMI when its "
@@ -311,7 +321,9 @@ def run(args) -> None:
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
     check(L.cgx_cg_set_mode(cg, args.mode))
     fused = args.mode == 2
-    mode_eff = 3 if args.mode == 0 else args.mode
+    me = C.c_int(0)
+    check(L.cgx_cg_get_mode(cg, C.byref(me)))
+    mode_eff = me.value
     total = args.warmup + args.steps + args.profile_steps
     check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total))
     bodies, stopped = C.c_int64(0), C.c_int(0)
@@ -341,7 +353,7 @@ def run(args) -> None:
     its = args.steps / elapsed
 
     # compulsory bytes of one iteration in the streamed formats, all ranks
-    spmv_fmt_local = sbytes.value + 16 * n_local  # matrix stream + p read + Ap written
+    spmv_fmt_local = spmv_bytes_per_iter(sbytes.value, n_local, mode_eff)
     iter_local = spmv_fmt_local + update_bytes_per_iter(n_local, mode_eff)
     if fused:
         iter_local = sbytes.value + 48 * n_local + 24 * n_local
@@ -365,18 +377,23 @@ def run(args) -> None:
     if calls[1] > 0:
         kb = spmv_fmt_local + (32 * n_local if fused else 0)
         ach = kb / (avg[1] * 1e-3) / 1e9
-        cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0)
+        cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
+            (16 * n_local if mode_eff == 4 else 0)
+        kname = {2: "k_spmv_fused", 4: "k_spmv_fd"}.get(mode_eff, "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_spmv_fused" if fused else "k_spmv_dot",
+                "kernel": kname,
                 "bytes_per_launch": kb,
                 "bytes_basis": "compulsory bytes of the kernel's own format: matrix stream "
-                               "(cgx_csr_stream_bytes) + p read + Ap written",
+                               "(cgx_csr_stream_bytes) + p read + Ap written" +
+                               (" + r read + p_k written" if mode_eff == 4 else ""),
                 "avg_us": round(avg[1] * 1e3, 2), "launches_timed": int(calls[1]),
                 "csr_equivalent_bytes_per_launch": cb,
                 "csr_equivalent_GBs": round(cb / (avg[1] * 1e-3) / 1e9, 1),
                 "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2)}}
-        if not fused:
+        if mode_eff == 4:  # once per 4 bodies
+            roof["other_kernels_avg_us"]["k_flush_group"] = round(avg[3] * 1e3, 2)
+        elif not fused:
             roof["other_kernels_avg_us"]["k_update_p"] = round(avg[3] * 1e3, 2)
         pmc = os.path.join(ROOT, "profiles", "pmc_spmv_dot.json")
         if os.path.exists(pmc):
@@ -432,9 +449,11 @@ def run(args) -> None:
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
                        "peer_fallback_reason": peer_note,
-                       "iteration": {0: "3 kernels, x update deferred over 4 bodies (auto)",
-                                     1: "3 kernels", 2: "fused (2 kernels)",
-                                     3: "3 kernels, x update deferred over 4 bodies"}[args.mode],
+                       "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
+                                     3: "3 kernels, x update deferred over 4 bodies",
+                                     4: "2 kernels (p update in the SpMV), x update deferred "
+                                        "over 4 bodies"}[mode_eff] +
+                                    (" (auto)" if args.mode == 0 else ""),
                        "spmv_variant": int(variant.value)},
             "roofline": roof,
             "csr_general": general,
@@ -472,6 +491,7 @@ def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):
         cg = C.c_void_p()
         check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
         check(L.cgx_cg_config(cg, args.poll, 1))
+        check(L.cgx_cg_set_mode(cg, mode_eff))
         check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 10 + steps + prof))
         bodies, stopped = C.c_int64(0), C.c_int(0)
         check(L.cgx_cg_run(cg, 10, C.byref(bodies), C.byref(stopped)))
@@ -487,7 +507,7 @@ def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):
         check(L.cgx_cg_kernel_times(cg, avg, calls))
         check(L.cgx_cg_destroy(cg))
         its = steps / (t1 - t0)
-        kb = sb.value + 16 * n
+        kb = spmv_bytes_per_iter(sb.value, n, mode_eff)
         it_b = kb + update_bytes_per_iter(n, mode_eff)
         out[name] = {"spmv_variant": int(v.value), "iterations_per_s": round(its, 2),
                      "GBs": round(it_b * its / 1e9, 1),

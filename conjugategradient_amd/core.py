@@ -359,7 +359,8 @@ class CG:
         self.final_rxr = float("nan")  # extension: rxr after the last body
         self.poll_every = 32
         self.use_graph = True
-        self.mode = 0  # cgx_cg_set_mode: 0 auto (= 3), 1 three kernels, 2 fused, 3 deferred x
+        self.mode = 0  # cgx_cg_set_mode: 0 auto (4 or 3), 1 three kernels, 2 fused, 3 deferred x,
+        # 4 fused + deferred x
 
     @classmethod
     def createCG(cls, dtype=np.float64, debug=Debuglevel.None_, device: int = 0) -> "CG":

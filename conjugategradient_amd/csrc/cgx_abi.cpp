@@ -133,7 +133,7 @@ template <class F> int timed(cgx_cg *cg, int kid, hipStream_t s, F &&launch) {
 // iterations after the stop return at entry and would skew the averages.
 int harvest_events(cgx_cg *cg, int64_t active_iters) {
   int64_t iter_seen = 0;
-  const int last_kid = cg->fused ? 2 : 3;
+  const int last_kid = (cg->fused || cg->fdefer) ? 2 : 3;
   for (auto &pr : cg->ev_pending) {
     const int kid = pr.first;
     float ms = 0;
@@ -286,6 +286,38 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   return CGX_OK;
 }
 
+// Fused deferred-x iteration (mode 4, single device): two kernels per body.
+// Kernel 1 computes p_k = r + beta p_{k-1} where the SpMV reads it and
+// stores it into P[k mod 4] (no separate p update: one read of p less per
+// body), kernel 2 is update_r with the stop rule; in slot 3 the group's x
+// updates are applied from the four p buffers (k_flush_group). Same values
+// as modes 1 and 3, bit for bit.
+template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
+  cgx_csr *A = cg->A;
+  hipStream_t s = cg->ctx->stream;
+  auto *st = (CgScalars<T> *)cg->st;
+  auto *ws = (RedWs<T> *)cg->ws;
+  T *P[4] = {(T *)cg->p, (T *)cg->pk[0], (T *)cg->pk[1], (T *)cg->pk[2]};
+  T *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
+  int rc;
+  const int npr = Launch<T>::update_parts(cg->n);
+  const int npp = Launch<T>::fd_parts(A->dev);
+  const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
+  if ((rc = timed(cg, 1, s, [&] {
+         return Launch<T>::spmv_fd(A->dev, r, P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, npr,
+                                   s, par);
+       })))
+    return rc;
+  if ((rc = timed(cg, 2, s, [&] {
+         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, npp, rpar, nullptr, 1);
+       })))
+    return rc;
+  if (slot == 3 &&
+      (rc = timed(cg, 3, s, [&] { return Launch<T>::flush_group(cg->n, x, P, st, s, rpar); })))
+    return rc;
+  return CGX_OK;
+}
+
 // Fused iteration (single device): x/p update folded into the next SpMV.
 template <typename T> int enqueue_iter_fused(cgx_cg *cg, int slot) {
   cgx_csr *A = cg->A;
@@ -307,6 +339,9 @@ template <typename T> int enqueue_iter_fused(cgx_cg *cg, int slot) {
 }
 
 int enqueue_iter_any(cgx_cg *cg, int slot) {
+  if (cg->fdefer)
+    return cg->dtype == CGX_F32 ? enqueue_iter_fdefer<float>(cg, slot)
+                                : enqueue_iter_fdefer<double>(cg, slot);
   if (cg->defer)
     return cg->dtype == CGX_F32 ? enqueue_iter_defer<float>(cg, slot)
                                 : enqueue_iter_defer<double>(cg, slot);
@@ -319,6 +354,28 @@ int enqueue_iter_any(cgx_cg *cg, int slot) {
 // Fused mode leaves the last body's x update pending, mode 3 up to three:
 // apply them (idempotent).
 int flush_pending_x(cgx_cg *cg) {
+  if (cg->fdefer) {
+    // bodies of an unfinished group (a finished one was applied by its slot-3
+    // flush), then the final r.r record when the run ended on an active body
+    hipStream_t s = cg->ctx->stream;
+    const int npr = cg->dtype == CGX_F32 ? Launch<float>::update_parts(cg->n)
+                                         : Launch<double>::update_parts(cg->n);
+    if (cg->dtype == CGX_F32) {
+      float *P[4] = {(float *)cg->p, (float *)cg->pk[0], (float *)cg->pk[1], (float *)cg->pk[2]};
+      if (cg->slot != 0)
+        CGX_HIP(Launch<float>::flush_defer(cg->n, (float *)cg->x, P, (CgScalars<float> *)cg->st, s));
+      CGX_HIP(Launch<float>::rr_settle((CgScalars<float> *)cg->st, (RedWs<float> *)cg->ws, npr, s));
+    } else {
+      double *P[4] = {(double *)cg->p, (double *)cg->pk[0], (double *)cg->pk[1],
+                      (double *)cg->pk[2]};
+      if (cg->slot != 0)
+        CGX_HIP(Launch<double>::flush_defer(cg->n, (double *)cg->x, P,
+                                            (CgScalars<double> *)cg->st, s));
+      CGX_HIP(Launch<double>::rr_settle((CgScalars<double> *)cg->st, (RedWs<double> *)cg->ws, npr,
+                                        s));
+    }
+    return CGX_OK;
+  }
   if (cg->defer) {
     hipStream_t s = cg->ctx->stream;
     if (cg->dtype == CGX_F32) {
@@ -1617,25 +1674,50 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
   cg->altdir = true;
   if (const char *e = std::getenv("CGX_ALTDIR")) cg->altdir = std::atoi(e) != 0;
   *out = cg;
-  // auto mode: three kernels with the x update deferred (mode 3: +4-8% over
-  // mode 1 at 256^3, fused measured slower); plain three
-  // kernels when the three extra p buffers do not fit
-  if (cgx_cg_set_mode(cg, 0) != CGX_OK) cg->defer = false;
+  // auto mode: the x update deferred over four p buffers, in three kernels
+  // (mode 3: +4-8% over mode 1 at 256^3) or, where it pays,
+  // two (mode 4, fd_auto); plain three kernels when the three extra p buffers
+  // do not fit
+  if (cgx_cg_set_mode(cg, 0) != CGX_OK) cg->defer = cg->fdefer = false;
   return CGX_OK;
+}
+
+// Auto mode picks 4 (fused deferred-x) where its kernel 1 adds no gathers
+// or the iteration is launch-bound, 3 elsewhere (profiles/r02_fd_*.log):
+//   * the 2-D plane march (gathers none: +-D from registers, +-1 from lanes):
+//     4096^2 4,927 against 4,632 it/s;
+//   * cache-resident stencil matrices (under 64 MB of CSR, the small-matrix
+//     rule's stencil form): two launches per body instead of three, 128^2
+//     96.7k against 80.0k it/s;
+// and not where kernel 1 doubles real gathers: 256^3 3,700 against 4,210,
+// 512^3 405 against 467, the G3 stand-in (CSR-stream) 19.96k against 22.5k.
+static bool fd_auto(const cgx_cg *cg) {
+  const cgx_csr *A = cg->A;
+  if (A->dist || cg->dtype != CGX_F64 || !Launch<double>::fd_supported(A->dev)) return false;
+  if (const char *e = std::getenv("CGX_AUTO_FD")) return std::atoi(e) != 0;  // A/B
+  const int v = launch_variant(A->dev, cg->dtype);
+  const bool march2d = (v & 2097152) && A->dev.march_a == 0;
+  const bool small = A->dev.nnz * (int64_t)(sizeof(double) + sizeof(int)) < (int64_t(64) << 20);
+  return march2d || (small && (v & 1048576));
 }
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
-  CGX_REQUIRE(mode >= 0 && mode <= 3, CGX_EINVAL,
-              "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x", mode);
-  CGX_REQUIRE(!(mode == 2 && cg->A->dist), CGX_EUNSUPPORTED,
-              "the fused iteration runs on a single device (partitioned matrices use mode 1)");
-  const bool f = mode == 2, d = mode == 3 || mode == 0;
-  if (f != cg->fused || d != cg->defer) {
+  CGX_REQUIRE(mode >= 0 && mode <= 4, CGX_EINVAL,
+              "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
+              "4 fused with deferred x", mode);
+  CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
+              "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
+  CGX_REQUIRE(mode != 4 || (cg->dtype == CGX_F64 && Launch<double>::fd_supported(cg->A->dev)),
+              CGX_EUNSUPPORTED, "mode 4 needs an f64 matrix in a production SpMV format "
+              "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
+  if (mode == 0) mode = fd_auto(cg) ? 4 : 3;
+  const bool f = mode == 2, d = mode == 3, fd = mode == 4;
+  if (f != cg->fused || d != cg->defer || fd != cg->fdefer) {
     CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
     drop_graph(cg);
   }
-  if (d && !cg->pk[0]) {  // three more p buffers (with the ghost tail when partitioned)
+  if ((d || fd) && !cg->pk[0]) {  // three more p buffers (with the ghost tail when partitioned)
     DeviceGuard g(cg->ctx->device);
     const size_t bytes = (size_t)(cg->n + cg->A->halo.n_ghost) * dtype_size(cg->dtype);
     for (int k = 0; k < 3; ++k) {
@@ -1653,6 +1735,25 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   }
   cg->fused = f;
   cg->defer = d;
+  cg->fdefer = fd;
+  return CGX_OK;
+}
+
+// mode 4's kernel 1 grid against the SpMV's (equal: mode 4 == mode 1 bit
+// for bit; else the p.Ap partials split differently)
+extern "C" int cgx_csr_fd_grid(cgx_csr *A, int *fd_grid, int *spmv_grid) {
+  CGX_REQUIRE(A && fd_grid && spmv_grid, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(A->dtype == CGX_F64 && Launch<double>::fd_supported(A->dev), CGX_EUNSUPPORTED,
+              "no mode-4 kernel for this matrix");
+  DeviceGuard g(A->ctx->device);
+  *fd_grid = Launch<double>::fd_parts(A->dev);
+  *spmv_grid = Launch<double>::spmv_parts(A->dev);
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_get_mode(cgx_cg *cg, int *mode) {
+  CGX_REQUIRE(cg && mode, CGX_EINVAL, "NULL argument");
+  *mode = cg->fdefer ? 4 : cg->defer ? 3 : cg->fused ? 2 : 1;
   return CGX_OK;
 }
 
@@ -1698,6 +1799,8 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
   cg->x = x;
   if (cg->fused)  // p_{-1} = 0 for body 0 of the fused iteration
     CGX_HIP(hipMemsetAsync(cg->p2, 0, (size_t)cg->n * dtype_size(cg->dtype), s));
+  if (cg->fdefer)  // mode 4: body 0 reads p_{-1} = P[3] (times beta = 0)
+    CGX_HIP(hipMemsetAsync(cg->pk[2], 0, (size_t)cg->n * dtype_size(cg->dtype), s));
   const void *xe = x;
   int rc;
   if (A->dist) {

@@ -154,7 +154,18 @@ template <typename T> struct Launch {
   // np_pap > 0: p.Ap from the spmv_dot partials; 0: from st->pAp[slot]
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0,
-                             int rev = 0, const T *rin = nullptr);  // rin: r_old (null: r)
+                             int rev = 0, const T *rin = nullptr,  // rin: r_old (null: r)
+                             int rule = 0);  // mode 4: the stop rule runs here
+  // mode 4 (fused deferred-x iteration, cgx_abi.cpp enqueue_iter_fdefer):
+  // kernel 1 computes p_k = r + beta p_{k-1} into pc where the SpMV reads it
+  static bool fd_supported(const CsrDev &A);
+  static int fd_parts(const CsrDev &A);  // kernel 1's grid (its p.Ap partials)
+  static hipError_t spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc, T *Ap,
+                            CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
+                            hipStream_t s, int rev = 0);
+  static hipError_t flush_group(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
+                                hipStream_t s, int rev = 0);
+  static hipError_t rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s);
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
   // SpMV + p.Ap over `count` SELL slices listed at `list` (device), partials

@@ -1942,6 +1942,60 @@ template <typename T> struct EpiFused {
     }
   }
 };
+// Fused deferred-x iteration (mode 4), the SpMV's epilogue: p_k = r_k +
+// beta_{k-1} p_{k-1} (CG.hpp:418 of body k-1) is computed where the SpMV
+// reads it (GatherP, also for the center pair the value-code forms hand to
+// pre2c) and stored once into this body's p buffer; then helper = A p_k and
+// value2 += helper.p_k (CG.hpp:374-379) exactly as EpiDot.
+template <typename T> struct EpiFD {
+  T *__restrict__ Ap;
+  T *__restrict__ pc;
+  GatherP<T> g;
+  T acc, pv, pv1;
+  __device__ __forceinline__ void pre(int i) { pv = g(i); }
+  __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
+    pv = c0;
+    pv1 = c1;
+  }
+  __device__ __forceinline__ void row(int i, T s) {
+    pc[i] = pv;
+    Ap[i] = s;
+    acc += s * pv;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    if (i1 == i0 + 1) {
+      const auto v = g.pair(i0);
+      pv = v.x;
+      pv1 = v.y;
+    } else {
+      pv = g(i0);
+      pv1 = g(i1);
+    }
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    using PV = typename PairOf<T>::V;
+    if (l0 && l1 && (((uintptr_t)(Ap + i)) & (sizeof(PV) - 1)) == 0) {  // pair stores
+      PV a, q;
+      a.x = s0;
+      a.y = s1;
+      q.x = pv;
+      q.y = pv1;
+      *reinterpret_cast<PV *>(Ap + i) = a;
+      *reinterpret_cast<PV *>(pc + i) = q;
+    } else {
+      if (l0) {
+        Ap[i] = s0;
+        pc[i] = pv;
+      }
+      if (l1) {
+        Ap[i + 1] = s1;
+        pc[i + 1] = pv1;
+      }
+    }
+    if (l0) acc += s0 * pv;
+    if (l1) acc += s1 * pv1;
+  }
+};
 template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
@@ -2026,6 +2080,68 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
 }
 
+// Fused deferred-x iteration (mode 4), kernel 1 of 2 for body k in slot s
+// (cgx_abi.cpp enqueue_iter_fdefer): p_k into P[s] from r and P[s-1] (EpiFD),
+// helper = A p_k, this workgroup's p.Ap partial. beta_{k-1} = r.r / rxr from
+// body k-1's update_r partials, summed in sum_parts order as
+// k_update_p_defer does, so every value is the one of modes 1 and 3; body 0
+// (bodies == 0) takes beta = 0 against a zeroed P[3]. Workgroup 0 records
+// rxr[s] (the r.r body k starts with) — also in the first skipped body,
+// where the host reads the final r.r — and, in slot 0, opens a new group of
+// deferred x updates (ran[] cleared; the slot-3 flush has applied the last).
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd(
+    CsrArgs A, const T *__restrict__ val, const T *__restrict__ r, const T *__restrict__ pold,
+    T *__restrict__ pc, T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
+    int np_rr) {
+  __shared__ LdsOf<T, V> sm;
+  const int prev = (slot + 3) & 3;
+  const long long bodies = st->bodies;
+  const bool act = st->active[slot] != 0;
+  if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+  if (!act) {
+    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot) {
+      const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+      if (threadIdx.x == 0) {
+        st->rr[prev] = rr;
+        st->rxr[slot] = rr;
+      }
+    }
+    return;
+  }
+  T beta = T(0);
+  if (bodies > 0) {
+    const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+    beta = rr / st->rxr[prev];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->rr[prev] = rr;  // the record
+      st->rxr[slot] = rr;
+    }
+  }
+  const GatherP<T> g{r, pold, beta};
+  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_any<T, V>(A, val, g, e, sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
+// The final r.r of a mode-4 run that ended on an active body (no kernel 1
+// followed to record it): rxr[s] of the next slot, as k_spmv_fd records it.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr) {
+  __shared__ T red[4 * kMaxRed];
+  const long long bodies = st->bodies;
+  if (bodies <= 0) return;
+  const int slot = (int)(bodies & 3);
+  const T rr = sum_parts(ws->rr_part, np_rr, red);
+  if (threadIdx.x == 0) {
+    st->rr[(slot + 3) & 3] = rr;
+    st->rxr[slot] = rr;
+  }
+}
+
 // Fused iteration, kernel 1 of 2 (slot s of body k). Reads active[s] (run
 // body k), xpend[s-1] (the x update of body k-1 is still pending) and
 // bodies == 0 (body 0: p_{-1} = 0, beta = 0). With body k inactive it only
@@ -2108,9 +2224,13 @@ template <typename T, bool FUSED>
 __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T *r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
-                                                     RedWs<T> *ws, int np_pap, int rev) {
+                                                     RedWs<T> *ws, int np_pap, int rev,
+                                                     int rule) {
+  // rule (mode 4, kernel 2 of 2): this kernel also runs the stop rule
+  // (CG.hpp:396-404, 436: on the r.r the body started with, which k_spmv_fd
+  // recorded) and marks the body's x update pending (ran[slot])
   if (!st->active[slot]) {
-    if (FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
+    if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
     return;
   }
   __shared__ T red[4];
@@ -2148,6 +2268,15 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
     st->pAp[slot] = pAp;
     st->alpha[slot] = alpha;
     st->skip[slot] = 0;
+    if (rule) {  // stop rule, as k_update_xp
+      const long long m = st->bodies + 1;
+      st->bodies = m;
+      const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
+      const bool cont = !cond && m < st->cap;
+      st->active[(slot + 1) & 3] = cont ? 1 : 0;
+      st->stopped = cond ? 1 : (cont ? 0 : 2);
+      st->ran[slot] = 1;
+    }
   }
   T acc = T(0);
   for (bool first = true; i + 3 * stride < n2; i += 4 * stride, first = false) {
@@ -2687,6 +2816,64 @@ __global__ __launch_bounds__(kBlock) void k_flush_defer(int64_t n, T *__restrict
   }
 }
 
+// Mode 4, slot 3 (after the body's update_r): the group's deferred x
+// updates, x = (((x + a0 p0) + a1 p1) + a2 p2) + a3 p3 over the slots that
+// ran in this group and no end-of-run flush applied (k_flush_defer's rule;
+// k_spmv_fd of the next slot 0 clears ran[]). 16-byte lanes; x and the p
+// buffers are not re-read before the next group overwrites them.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict__ x,
+                                                        const T *__restrict__ P0,
+                                                        const T *__restrict__ P1,
+                                                        const T *__restrict__ P2,
+                                                        const T *__restrict__ P3,
+                                                        const CgScalars<T> *st, int rev) {
+  T a[4];
+  bool use[4];
+  bool any = false;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    a[t] = st->alpha[t];
+    use[t] = st->ran[t] != 0 && st->skip[t] == 0;
+    any = any || use[t];
+  }
+  if (!any) return;
+  using V = typename Vec2<T>::V;
+  const int64_t n2 = n >> 1;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  V *x2 = reinterpret_cast<V *>(x);
+  const V *Q[4] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
+                   reinterpret_cast<const V *>(P2), reinterpret_cast<const V *>(P3)};
+  auto body = [&](int64_t i) {
+    V xv = ldv<kStreamNt, T>(x2 + i);
+    V q[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) q[t] = ldv<kStreamNt, T>(Q[t] + i);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (use[t]) {
+        xv.x = xv.x + a[t] * q[t].x;
+        xv.y = xv.y + a[t] * q[t].y;
+      }
+    }
+    stv<kStreamNt, T>(x2 + i, xv);
+  };
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + stride < n2; i += 2 * stride) {
+    body(E(i));
+    body(E(i + stride));
+  }
+  for (; i < n2; i += stride) body(E(i));
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    T xv = x[n - 1];
+    const T *Ps[4] = {P0, P1, P2, P3};
+    for (int t = 0; t < 4; ++t)
+      if (use[t]) xv = xv + a[t] * Ps[t][n - 1];
+    x[n - 1] = xv;
+  }
+}
+
 // *dst = sum of part[0..np) in sum_parts order (partitioned runs: the local
 // dot before its RCCL all-reduce)
 template <typename T>
@@ -2947,17 +3134,99 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                                RedWs<T> *ws, hipStream_t s, bool fused, int np_pap, int rev,
-                               const T *rin) {
+                               const T *rin, int rule) {
   if (!rin) rin = r;
   if (fused) {
     hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n, kMaxGrid)), dim3(kBlock), 0, s,
                        n, rin, r,
-                       Ap, st, slot, ws, 0, 0);
+                       Ap, st, slot, ws, 0, 0, 0);
   } else {
     hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
-                       s, n, rin, r, Ap, st, slot, ws, np_pap, rev);
+                       s, n, rin, r, Ap, st, slot, ws, np_pap, rev, rule);
   }
   return hipGetLastError();
+}
+
+// ---- mode 4 (fused deferred-x iteration): k_spmv_fd is instantiated for
+// the production SpMV forms only (CSR-stream, SELL-P, value-code SELL-P and
+// its pipelined / stencil / plane-march loops), f64 only; other variants
+// keep mode 3 (fd_supported).
+#define CGX_FD_LIST(X)                                                                 \
+  X(13) X(15) X(8192) X(8194) X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) \
+  X(827392) X(827394) X(1613824) X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) \
+  X(3973120) X(3973122)
+
+template <typename T> static const void *spmv_fd_kernel(int v) {
+  if constexpr (!std::is_same<T, double>::value) {
+    (void)v;
+    return nullptr;
+  } else {
+    switch (v) {
+#define CGX_KF(VV) \
+  case VV: return reinterpret_cast<const void *>(&k_spmv_fd<T, VV>);
+      CGX_FD_LIST(CGX_KF)
+#undef CGX_KF
+      default: return nullptr;
+    }
+  }
+}
+
+// resident workgroups of k_spmv_fd<v> (0: unknown), as spmv_dot_resident
+template <typename T> static int spmv_fd_resident(int v) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, v});
+  if (it != cache.end()) return it->second;
+  int res = 0;
+  if (const void *k = spmv_fd_kernel<T>(v)) {
+    int nb = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      res = nb * cus;
+  }
+  cache[{dev, v}] = res;
+  return res;
+}
+
+template <typename T> bool Launch<T>::fd_supported(const CsrDev &A) {
+  return spmv_fd_kernel<T>(spmv_variant<T>(A)) != nullptr;
+}
+// k_spmv_fd's grid: the SpMV's (grid_rows) capped at its own resident
+// workgroups. It carries more VGPRs than k_spmv_dot (e.g. 107 against 96,
+// 147 against 124), so on a matrix big enough to fill the chip the cap is
+// lower and the p.Ap partials split differently: mode 4 then equals mode 1
+// to rounding (the sum order of one dot), not bit for bit. Holding k_spmv_fd
+// to k_spmv_dot's waves per SIMD instead spilled 20-56 VGPRs to scratch.
+template <typename T> int Launch<T>::fd_parts(const CsrDev &A) {
+  const int grid = grid_rows(A.nrb);
+  const int r = spmv_fd_resident<T>(spmv_variant<T>(A));
+  return (r > 0 && r < grid) ? r : grid;
+}
+template <typename T>
+hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc, T *Ap,
+                              CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
+                              hipStream_t s, int rev) {
+  const void *k = spmv_fd_kernel<T>(spmv_variant<T>(A));
+  if (!k) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  const T *val = (const T *)A.val;
+  void *kargs[] = {&a, (void *)&val, (void *)&r, (void *)&pold, (void *)&pc, (void *)&Ap,
+                   (void *)&st, (void *)&slot, (void *)&ws, (void *)&np_rr};
+  return hipLaunchKernel(k, dim3(fd_parts(A)), dim3(kBlock), kargs, 0, s);
+}
+template <typename T>
+hipError_t Launch<T>::flush_group(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
+                                  hipStream_t s, int rev) {
+  CGX_LAUNCH(k_flush_group<T>, grid_elems(n, kGridUpdateP), n, x, (const T *)P[0],
+             (const T *)P[1], (const T *)P[2], (const T *)P[3], (const CgScalars<T> *)st, rev);
+}
+template <typename T>
+hipError_t Launch<T>::rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s) {
+  CGX_LAUNCH(k_rr_settle<T>, 1, st, ws, np_rr);
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
   return cap_resident<T>(grid_rows(A.nrb), spmv_variant<T>(A));  // = spmv_dot's grid

@@ -165,6 +165,7 @@ struct cgx_cg {
   void *p2 = nullptr;   // second p buffer of the fused iteration (single device)
   bool fused = false;   // two kernels per iteration (x/p update folded into SpMV)
   bool defer = false;   // mode 3: x updated once per 4 bodies from 4 p buffers
+  bool fdefer = false;  // mode 4: p update folded into the SpMV, x deferred as mode 3
   bool altdir = false;  // alternate the kernels' sweep directions (Infinity-Cache reuse)
   void *pk[3] = {nullptr, nullptr, nullptr};  // p buffers 1..3 of mode 3 (n + n_ghost)
   void *st = nullptr;   // cgx::CgScalars<T>

@@ -158,7 +158,8 @@ int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable);
 int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
 /* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
 int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
-/* Iteration structure (before cgx_cg_begin): 0 auto (= 3, the default), 1
+/* Iteration structure (before cgx_cg_begin): 0 auto (4 for the 2-D plane
+ * march and cache-resident stencil matrices, else 3; the default), 1
  * three kernels
  * (SpMV+p.Ap, r-update+r.r, x/p-update), 2 fused (single device only): two
  * kernels, the x/p update folded into the next iteration's SpMV (p_j =
@@ -166,8 +167,19 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * twice the gathers; 3 three kernels with the x update deferred: p cycles
  * through four buffers and x += a0 p0 + ... + a3 p3 (in order) runs once
  * per four bodies and at the end of each cgx_cg_run (34 N instead of 40 N
- * bytes per body for the x/p update). All modes give bit-identical x. */
+ * bytes per body for the x/p update); 4 fused with deferred x (single
+ * device, f64, production SpMV formats): two kernels per body, p_k = r +
+ * beta p_{k-1} computed where the SpMV reads it and stored once into the
+ * p ring, update_r with the stop rule, x from the four p buffers in slot 3
+ * (72 N + matrix bytes per body against 78 N in mode 3).
+ * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
+ * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
+/* the iteration structure in effect (1-4; auto resolved) */
+int cgx_cg_get_mode(cgx_cg *cg, int *mode);
+/* mode 4's fused SpMV grid and the SpMV's: where they are equal mode 4 is
+ * bit-identical to mode 1, else equal to rounding (one dot's sum order) */
+int cgx_csr_fd_grid(cgx_csr *A, int *fd_grid, int *spmv_grid);
 
 /* CG::accuracy (CG.hpp:463-515): blocking; |sum (b-Ax)^2 / sum x^2|. */
 int cgx_accuracy(cgx_ctx *ctx, cgx_csr *A, const void *d_b, const void *d_x,

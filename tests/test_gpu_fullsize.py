@@ -13,7 +13,9 @@ golden cases:
     the reference iteration at ||dx|| / ||x|| <= 1e-10 — the dots are
     reductions in another order, so this is the floating-point bar of
     SURVEY §8(c) —, and the deferred-x iteration (mode 3) is bit-identical
-    to the three-kernel one (mode 1): a size-independent property.
+    to the three-kernel one (mode 1): a size-independent property (mode 4:
+    to rounding, see test_gpu_fdefer.py). The solve to tolerance runs the
+    auto mode (4 at 4096^2, 3 at 256^3).
 """
 import ctypes as C
 
@@ -82,6 +84,10 @@ def test_fullsize_cg_bodies_match_oracle(queue, oracle, full):
     assert rel(x3, xr) <= 1e-10, (name, rel(x3, xr))
     x1 = _bodies(queue, m, b, 1).extract()
     np.testing.assert_array_equal(x3, x1)
+    # mode 4 (p update folded into the SpMV; auto at 4096^2): its SpMV has
+    # fewer resident workgroups here, so p.Ap sums in another order
+    x4 = _bodies(queue, m, b, 4).extract()
+    assert rel(x4, x1) <= 1e-11 and rel(x4, xr) <= 1e-10
     # accuracy() (CG.hpp:463-515) of the device x against the oracle's formula
     acc = cg3.accuracy()
     assert acc == pytest.approx(oracle.accuracy(rp, cl, vl, b, x3), rel=1e-9)
