@@ -166,13 +166,27 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
   if (halo && A->peer.on) {
     // device peer transport: push p's boundary entries into the neighbours,
     // run the interior slices, wait for the neighbours' entries, then the
-    // boundary slices (or wait, then one launch when the matrix is not split)
-    if ((rc = peer_push<T>(A, p, st, slot, s))) return rc;
+    // boundary slices (or wait, then one launch when the matrix is not split).
+    // A split SELL matrix carries the push in the interior launch's first
+    // workgroups (k_spmv_dot_push: the xGMI stores overlap the interior
+    // slices, one launch less; $CGX_PEER_PUSH_MERGE=0 keeps k_peer_push)
     const bool split = A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192));
-    const int gi = split ? Launch<T>::slice_grid(A->dev, A->split_ni) : 0;
+    const int wg0 = A->peer.dev.nsend * kPushWG;
+    static const bool merge_on = [] {
+      const char *e = std::getenv("CGX_PEER_PUSH_MERGE");
+      return !e || std::atoi(e) != 0;
+    }();
+    const bool merged = split && wg0 > 0 && merge_on && Launch<T>::push_supported(A->dev);
+    if (!merged && (rc = peer_push<T>(A, p, st, slot, s))) return rc;
+    const int gi = !split ? 0
+                   : merged ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
+                            : Launch<T>::slice_grid(A->dev, A->split_ni);
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = hipSuccess;
-           if (split)
+           if (merged)
+             e = Launch<T>::spmv_dot_slices_push(A->dev, A->d_split, A->split_ni, 0, p, Ap, st,
+                                                 slot, ws, s, rev, A->peer.dev, wg0);
+           else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
            if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
@@ -215,12 +229,25 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
 // A partitioned run's dot: the local partials summed, then all-reduced into
 // *dst — by the device peer transport in one kernel, or finalized into the
 // scalar ring and all-reduced by the setup transport (RCCL / host).
-template <typename T> int dist_dot(cgx_cg *cg, const T *part, int np, T *dst, int slot) {
+template <typename T>
+int dist_dot(cgx_cg *cg, const T *part, int np, T *dst, int slot, int which) {
   hipStream_t s = cg->ctx->stream;
   if (cg->A->peer.on)
-    return peer_allreduce<T>(cg->A, part, np, dst, (CgScalars<T> *)cg->st, slot, s);
+    return peer_allreduce<T>(cg->A, part, np, dst, (CgScalars<T> *)cg->st, slot, s, which);
   CGX_HIP(Launch<T>::finalize(part, np, dst, s));
   return dist_allreduce_scalar(cg->ctx, dst, cg->dtype, 1, s);
+}
+
+// The device peer transport's two all-reduces of a body run inside the
+// kernels that consume them (update_r: p.Ap, the x/p update: r.r; every
+// workgroup polls the mailboxes, peerdev::world_sum) instead of as two
+// one-workgroup launches; $CGX_PEER_AR_FUSE=0 keeps k_peer_allreduce.
+static const PeerDev *fused_ar(const cgx_cg *cg) {
+  static const bool on = [] {
+    const char *e = std::getenv("CGX_PEER_AR_FUSE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return (on && cg->A->dist && cg->A->peer.on) ? &cg->A->peer.dev : nullptr;
 }
 
 template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
@@ -237,16 +264,18 @@ template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
   // sweep directions: each kernel starts where the previous one ended
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
   int npp = 0;
+  const PeerDev *far = fused_ar(cg);
+  const bool sep = A->dist && !far;  // a separate all-reduce step per dot
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
-  if (A->dist && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot))) return rc;
+  if (sep && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot, 1))) return rc;
   if ((rc = timed(cg, 2, s, [&] {
-         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp,
-                                    rpar);
+         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, sep ? 0 : npp, rpar,
+                                    nullptr, 0, far);
        })))
     return rc;
-  if (A->dist && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot))) return rc;
+  if (sep && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot, 2))) return rc;
   if ((rc = timed(cg, 3, s, [&] {
-         return Launch<T>::update_xp(cg->n, x, p, r, st, slot, ws, A->dist ? 0 : npr, s, par);
+         return Launch<T>::update_xp(cg->n, x, p, r, st, slot, ws, sep ? 0 : npr, s, par, far);
        })))
     return rc;
   return CGX_OK;
@@ -270,17 +299,19 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   // sweep directions: each kernel starts where the previous one ended
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
   int npp = 0;
+  const PeerDev *far = fused_ar(cg);
+  const bool sep = A->dist && !far;  // a separate all-reduce step per dot
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
-  if (A->dist && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot))) return rc;
+  if (sep && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot, 1))) return rc;
   if ((rc = timed(cg, 2, s, [&] {
-         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, A->dist ? 0 : npp,
-                                    rpar);
+         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, sep ? 0 : npp, rpar,
+                                    nullptr, 0, far);
        })))
     return rc;
-  if (A->dist && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot))) return rc;
+  if (sep && (rc = dist_dot<T>(cg, ws->rr_part, npr, &st->rr[slot], slot, 2))) return rc;
   if ((rc = timed(cg, 3, s, [&] {
-         return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, A->dist ? 0 : npr,
-                                          s, par);
+         return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, sep ? 0 : npr, s,
+                                          par, far);
        })))
     return rc;
   return CGX_OK;
@@ -1835,10 +1866,10 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
     // the init kernel left the local r.r in rxr[0]; all-reduce it in place
     if (cg->dtype == CGX_F32) {
       auto *st = (CgScalars<float> *)cg->st;
-      rc = peer_allreduce<float>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s);
+      rc = peer_allreduce<float>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s, 0);
     } else {
       auto *st = (CgScalars<double> *)cg->st;
-      rc = peer_allreduce<double>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s);
+      rc = peer_allreduce<double>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s, 0);
     }
     if (rc) return rc;
   } else if (A->dist) {

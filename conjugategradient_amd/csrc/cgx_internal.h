@@ -99,6 +99,8 @@ struct SellSlice {
   int width;     // entries per row in this slice (longest row)
 };
 
+struct PeerDev;  // cgx_objects.h
+
 // ---- launchers (cgx_kernels.hip) --------------------------------------------
 struct CsrDev {
   int64_t n, nnz;
@@ -155,7 +157,8 @@ template <typename T> struct Launch {
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0,
                              int rev = 0, const T *rin = nullptr,  // rin: r_old (null: r)
-                             int rule = 0);  // mode 4: the stop rule runs here
+                             int rule = 0,   // mode 4: the stop rule runs here
+                             const PeerDev *peer = nullptr);  // p.Ap all-reduced here
   // mode 4 (fused deferred-x iteration, cgx_abi.cpp enqueue_iter_fdefer):
   // kernel 1 computes p_k = r + beta p_{k-1} into pc where the SpMV reads it
   static bool fd_supported(const CsrDev &A);
@@ -174,6 +177,14 @@ template <typename T> struct Launch {
                                     const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
                                     hipStream_t s, int rev = 0);
   static int slice_grid(const CsrDev &A, int count);
+  // the same interior launch with the peer transport's halo push in its first
+  // wg0 workgroups (k_spmv_dot_push); slice_grid_push: its SpMV workgroups
+  static bool push_supported(const CsrDev &A);
+  static int slice_grid_push(const CsrDev &A, int count, int wg0);
+  static hipError_t spmv_dot_slices_push(const CsrDev &A, const int *list, int count,
+                                         int part_off, const T *p, T *Ap, CgScalars<T> *st,
+                                         int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                         const PeerDev &P, int wg0);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);
@@ -182,11 +193,15 @@ template <typename T> struct Launch {
   static hipError_t flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,
                             RedWs<T> *ws, hipStream_t s);
   // np_rr > 0: r.r from the update_r partials; 0: from st->rr[slot]
+  // peer: a partitioned run's r.r all-reduced in the kernel (device peer
+  // transport; np_rr the local partials)
   static hipError_t update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                              int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev = 0);
+                              int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev = 0,
+                              const PeerDev *peer = nullptr);
   static hipError_t update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
                                    const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
-                                   int np_rr, hipStream_t s, int rev = 0);
+                                   int np_rr, hipStream_t s, int rev = 0,
+                                   const PeerDev *peer = nullptr);
   static hipError_t flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                 hipStream_t s);
   static hipError_t dot_acc(int64_t n, const T *x, const T *y, T *res, RedWs<T> *ws,

@@ -29,6 +29,7 @@
 //    as in the reference's expressions.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -36,6 +37,8 @@
 #include <type_traits>
 
 #include "cgx_internal.h"
+#include "cgx_objects.h"
+#include "cgx_peer_dev.h"
 
 namespace cgx {
 namespace {
@@ -261,6 +264,10 @@ struct CsrArgs {
   // pattern), the pattern's +-a offset (0: 2-D form), its pool base, and
   // the run length in planes (0: fill the grid)
   int mk, mo, mpat, ml;
+  // leading workgroups of the launch that do something else (the halo push
+  // of k_spmv_dot_push): the SpMV's work split and partials use blockIdx -
+  // wg0 of gridDim - wg0 workgroups (a multiple of 8 keeps the XCD groups)
+  int wg0;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -989,19 +996,19 @@ template <typename T> struct SellLds {
 // The waves of one XCD walk a contiguous slice range (as variant bit 1);
 // consecutive slices on the waves of one workgroup. Slice indices fit int
 // (n < 2^31), which keeps the loop control on the scalar unit.
-__device__ __forceinline__ void sell_range(int nsl, int &first, int &step, int &end,
+__device__ __forceinline__ void sell_range(int nsl, int wg0, int &first, int &step, int &end,
                                            int &lo) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int G = gridDim.x;
+  const int G = (int)gridDim.x - wg0, b = (int)blockIdx.x - wg0;
   if ((G & 7) == 0) {
-    const int g = blockIdx.x & 7;
+    const int g = b & 7;
     lo = (int)(((int64_t)nsl * g) >> 3);
-    first = lo + (blockIdx.x >> 3) * 4 + wid;
+    first = lo + (b >> 3) * 4 + wid;
     end = (int)(((int64_t)nsl * (g + 1)) >> 3);
     step = (G >> 3) * 4;
   } else {
     lo = 0;
-    first = blockIdx.x * 4 + wid;
+    first = b * 4 + wid;
     end = nsl;
     step = G * 4;
   }
@@ -1059,7 +1066,7 @@ __device__ __forceinline__ int slice_at(const CsrArgs &A, int k) {
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell(const CsrArgs &A, const Gather &x, Epi &epi) {
   int s, step, end, lo;
-  sell_range((int)A.nsl, s, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   for (; s < end; s += step)
     sell_slice<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
@@ -1077,7 +1084,7 @@ __device__ __forceinline__ void spmv_sell_pipe(const CsrArgs &A, const Gather &x
   const T *__restrict__ sval = static_cast<const T *>(A.sval);
   const int lane = threadIdx.x & 63;
   int first, step, end, lo;
-  sell_range((int)A.nsl, first, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, first, step, end, lo);
   const int full = (int)(A.n / kSellRows);  // slices whose 64 rows all exist
   const int pend = min(end, full);
   auto issue = [&](int q, unsigned long long &iw, T(&v)[8], int &dv) {
@@ -1200,7 +1207,7 @@ __device__ __forceinline__ void sell_slice2(const CsrArgs &A, const Gather &x, E
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sell2(const CsrArgs &A, const Gather &x, Epi &epi) {
   int s, step, end, lo;
-  sell_range((int)A.nsl, s, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   for (; s < end; s += step)
     sell_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
@@ -1276,7 +1283,7 @@ __device__ __forceinline__ void sellp_slice2(const CsrArgs &A, const Gather &x, 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sellp(const CsrArgs &A, const Gather &x, Epi &epi) {
   int s, step, end, lo;
-  sell_range((int)A.nsl, s, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   for (; s < end; s += step)
     sellp_slice2<T, V, Epi, Gather>(A, x, epi, slice_at(A, A.rev ? lo + end - 1 - s : s));
 }
@@ -1412,7 +1419,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
   const int lane = threadIdx.x & 63;
   const int nxm2 = (int)A.nx - 2;
   int s, step, end, lo;
-  sell_range((int)A.nsl, s, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   if (s >= end) return;
   auto code_at = [&](int64_t coff) {
     Ull2 cw;
@@ -1616,7 +1623,7 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
   // byte offsets into x fit 32 bits (else every slice takes sellpv_slice2)
   const bool off32 = (uint64_t)A.nx * sizeof(T) < (uint64_t(1) << 32);
   int it, step, end, lo;
-  sell_range(K * Z, it, step, end, lo);
+  sell_range(K * Z, A.wg0, it, step, end, lo);
   auto code_at = [&](int sl) {
     Ull2 cw;
     if constexpr (C4) {
@@ -1786,7 +1793,7 @@ __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, E
     return;
   }
   int s, step, end, lo;
-  sell_range((int)A.nsl, s, step, end, lo);
+  sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   for (; s < end; s += step)
     sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd,
                                      slice_at(A, A.rev ? lo + end - 1 - s : s));
@@ -2080,6 +2087,29 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
 }
 
+// The interior SpMV of a partitioned SELL matrix with the device peer
+// transport's halo push in its first A.wg0 workgroups (peerdev::push_wg, as
+// k_peer_push): the push's xGMI stores overlap the interior slices instead
+// of running as a launch of their own before them. The SpMV workgroups are
+// k_spmv_dot's, renumbered from wg0 (sell_range), partials at
+// part_off + blockIdx - wg0.
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
+    CsrArgs A, const T *__restrict__ val, const T *__restrict__ p, T *__restrict__ Ap,
+    CgScalars<T> *st, int slot, RedWs<T> *ws, PeerDev P) {
+  if ((int)blockIdx.x < A.wg0) {
+    peerdev::push_wg<T>(p, P, st, slot, blockIdx.x);
+    return;
+  }
+  if (!st->active[slot]) return;
+  __shared__ LdsOf<T, V> sm;
+  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
+  spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+}
+
 // Fused deferred-x iteration (mode 4), kernel 1 of 2 for body k in slot s
 // (cgx_abi.cpp enqueue_iter_fdefer): p_k into P[s] from r and P[s-1] (EpiFD),
 // helper = A p_k, this workgroup's p.Ap partial. beta_{k-1} = r.r / rxr from
@@ -2219,13 +2249,24 @@ template <> struct Vec2<float> { using V = float2; };
 // r = r - alpha * Ap ; rr = r.r          (CG.hpp:381-393, 406-407)
 // FUSED: kernel 2 of 2 of the fused iteration, which also runs the stop rule
 // (CG.hpp:396-404, 410-417, 436) and marks body k's x update as pending.
-template <typename T, bool FUSED>
+// PEER (partitioned run, device peer transport): p.Ap from this rank's
+// partials, then all-reduced here (peerdev::world_sum, tag base + 1) instead
+// of by a k_peer_allreduce launch before this kernel.
+template <typename T> __device__ __forceinline__ void peer_fault(CgScalars<T> *st, int slot,
+                                                                 const PeerDev *P) {
+  if (threadIdx.x == 0) {
+    P->state->fault = 1;
+    st->active[slot] = 0;
+    st->stopped = 3;
+  }
+}
+
+template <typename T, bool FUSED, bool PEER>
 // rin == r: in place (modes 1, 2); else r ping-pongs between two buffers.
-__global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T *r,
-                                                     const T *__restrict__ Ap,
-                                                     CgScalars<T> *st, int slot,
-                                                     RedWs<T> *ws, int np_pap, int rev,
-                                                     int rule) {
+__device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
+                                              const T *__restrict__ Ap, CgScalars<T> *st,
+                                              int slot, RedWs<T> *ws, int np_pap, int rev,
+                                              int rule, const PeerDev *P) {
   // rule (mode 4, kernel 2 of 2): this kernel also runs the stop rule
   // (CG.hpp:396-404, 436: on the r.r the body started with, which k_spmv_fd
   // recorded) and marks the body's x update pending (ran[slot])
@@ -2262,7 +2303,18 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
     rv[u] = ri2[j];
     av[u] = ldv<kStreamNt, T>(a2 + j);  // Ap is dead after this kernel
   }
-  const T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
+  T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
+  if constexpr (PEER) {
+    __shared__ double wres;
+    __shared__ int wok;
+    if (P->state->fault) return;
+    if (!peerdev::world_sum((double)pAp, P->state->arb[slot & 1] + 1, *P, blockIdx.x == 0,
+                            &wres, &wok)) {
+      peer_fault(st, slot, P);
+      return;
+    }
+    pAp = (T)wres;
+  }
   const T alpha = rxr / pAp;
   if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) {  // the record; the deferred x update
     st->pAp[slot] = pAp;
@@ -2333,13 +2385,29 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
   }
 }
 
-// x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
+template <typename T, bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T *r,
+                                                     const T *__restrict__ Ap,
+                                                     CgScalars<T> *st, int slot,
+                                                     RedWs<T> *ws, int np_pap, int rev,
+                                                     int rule) {
+  update_r_body<T, FUSED, false>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule, nullptr);
+}
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__ x,
-                                                      T *__restrict__ p,
-                                                      const T *__restrict__ r,
-                                                      CgScalars<T> *st, int slot,
-                                                      RedWs<T> *ws, int np_rr, int rev) {
+__global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
+                                                          const T *__restrict__ Ap,
+                                                          CgScalars<T> *st, int slot,
+                                                          RedWs<T> *ws, int np_pap, int rev,
+                                                          PeerDev P) {
+  update_r_body<T, false, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
+}
+
+// x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
+template <typename T, bool PEER>
+__device__ __forceinline__ void update_xp_body(int64_t n, T *__restrict__ x, T *__restrict__ p,
+                                               const T *__restrict__ r, CgScalars<T> *st,
+                                               int slot, RedWs<T> *ws, int np_rr, int rev,
+                                               const PeerDev *P) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
@@ -2348,7 +2416,18 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
   __shared__ T red[4];
   const T rxr = st->rxr[slot];
   const T alpha = rxr / st->pAp[slot];
-  const T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+  T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+  if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
+    __shared__ double wres;
+    __shared__ int wok;
+    if (P->state->fault) return;
+    if (!peerdev::world_sum((double)rr, P->state->arb[slot & 1] + 2, *P, blockIdx.x == 0, &wres,
+                            &wok)) {
+      peer_fault(st, slot, P);
+      return;
+    }
+    rr = (T)wres;
+  }
   const T beta = rr / rxr;
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
@@ -2400,7 +2479,29 @@ __global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__
     st->active[nxt] = cont ? 1 : 0;
     st->rxr[nxt] = rr;
     st->stopped = cond ? 1 : (cont ? 0 : 2);
+    if constexpr (PEER) {  // the next body's tag base
+      const unsigned long long t = P->state->arb[slot & 1] + 2;
+      P->state->ar = t;
+      P->state->arb[(slot + 1) & 1] = t;
+    }
   }
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_update_xp(int64_t n, T *__restrict__ x,
+                                                      T *__restrict__ p,
+                                                      const T *__restrict__ r,
+                                                      CgScalars<T> *st, int slot,
+                                                      RedWs<T> *ws, int np_rr, int rev) {
+  update_xp_body<T, false>(n, x, p, r, st, slot, ws, np_rr, rev, nullptr);
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_update_xp_peer(int64_t n, T *__restrict__ x,
+                                                           T *__restrict__ p,
+                                                           const T *__restrict__ r,
+                                                           CgScalars<T> *st, int slot,
+                                                           RedWs<T> *ws, int np_rr, int rev,
+                                                           PeerDev P) {
+  update_xp_body<T, true>(n, x, p, r, st, slot, ws, np_rr, rev, &P);
 }
 
 // *res += x.y (dot_product_trivial / norm: accumulate, Q4)
@@ -2686,13 +2787,12 @@ template <typename T> int Launch<T>::grid_elems(int64_t n, int cap) {
 // 8 N + 8 N (x) + 24 N (p0..p2) bytes once instead of 16 N four times.
 // In slot 3, pn is P0 (p_{k+1} replaces p_{k-3}): every element's flush
 // operands are loaded before its stores, and pn / P0 carry no __restrict__.
-template <typename T, bool FLUSH>
-__global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restrict__ x,
-                                                           const T *p, T *pn, const T *P0,
-                                                           const T *P1, const T *P2,
-                                                           const T *__restrict__ r,
-                                                           CgScalars<T> *st, int slot,
-                                                           RedWs<T> *ws, int np_rr, int rev) {
+template <typename T, bool FLUSH, bool PEER>
+__device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x, const T *p,
+                                                    T *pn, const T *P0, const T *P1,
+                                                    const T *P2, const T *__restrict__ r,
+                                                    CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                                    int np_rr, int rev, const PeerDev *PD) {
   const int nxt = (slot + 1) & 3;
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
@@ -2700,7 +2800,18 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
   }
   __shared__ T red[4];
   const T rxr = st->rxr[slot];
-  const T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+  T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+  if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
+    __shared__ double wres;
+    __shared__ int wok;
+    if (PD->state->fault) return;
+    if (!peerdev::world_sum((double)rr, PD->state->arb[slot & 1] + 2, *PD, blockIdx.x == 0,
+                            &wres, &wok)) {
+      peer_fault(st, slot, PD);
+      return;
+    }
+    rr = (T)wres;
+  }
   const T beta = rr / rxr;
   // slot-3 flush: alphas and skips of the group, written by earlier launches
   T a[4] = {T(0), T(0), T(0), T(0)};
@@ -2782,7 +2893,30 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
     } else {
       st->ran[slot] = 1;
     }
+    if constexpr (PEER) {  // the next body's tag base
+      const unsigned long long t = PD->state->arb[slot & 1] + 2;
+      PD->state->ar = t;
+      PD->state->arb[(slot + 1) & 1] = t;
+    }
   }
+}
+template <typename T, bool FLUSH>
+__global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restrict__ x,
+                                                           const T *p, T *pn, const T *P0,
+                                                           const T *P1, const T *P2,
+                                                           const T *__restrict__ r,
+                                                           CgScalars<T> *st, int slot,
+                                                           RedWs<T> *ws, int np_rr, int rev) {
+  update_p_defer_body<T, FLUSH, false>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr, rev,
+                                       nullptr);
+}
+template <typename T, bool FLUSH>
+__global__ __launch_bounds__(kBlock) void k_update_p_defer_peer(
+    int64_t n, T *__restrict__ x, const T *p, T *pn, const T *P0, const T *P1, const T *P2,
+    const T *__restrict__ r, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr, int rev,
+    PeerDev PD) {
+  update_p_defer_body<T, FLUSH, true>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr, rev,
+                                      &PD);
 }
 
 // End of a run in mode 3: apply the bodies of the current group that ran and
@@ -3134,8 +3268,14 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
 template <typename T>
 hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                                RedWs<T> *ws, hipStream_t s, bool fused, int np_pap, int rev,
-                               const T *rin, int rule) {
+                               const T *rin, int rule, const PeerDev *peer) {
   if (!rin) rin = r;
+  if (peer) {
+    if (fused || rule || rin != r) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_update_r_peer<T>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
+                       s, n, r, Ap, st, slot, ws, np_pap, rev, *peer);
+    return hipGetLastError();
+  }
   if (fused) {
     hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n, kMaxGrid)), dim3(kBlock), 0, s,
                        n, rin, r,
@@ -3218,6 +3358,56 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
                    (void *)&st, (void *)&slot, (void *)&ws, (void *)&np_rr};
   return hipLaunchKernel(k, dim3(fd_parts(A)), dim3(kBlock), kargs, 0, s);
 }
+// ---- the interior SpMV with the halo push in front (k_spmv_dot_push): the
+// SELL forms a partitioned matrix takes (no plane march: slice lists)
+#define CGX_PUSH_LIST(X)                                                                \
+  X(2048) X(2050) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)  \
+  X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824) X(1613826)     \
+  X(1875968) X(1875970)
+
+template <typename T> static const void *spmv_push_kernel(int v) {
+  switch (v) {
+#define CGX_KPU(VV) \
+  case VV: return reinterpret_cast<const void *>(&k_spmv_dot_push<T, VV>);
+    CGX_PUSH_LIST(CGX_KPU)
+#undef CGX_KPU
+    default: return nullptr;
+  }
+}
+
+template <typename T> bool Launch<T>::push_supported(const CsrDev &A) {
+  return spmv_push_kernel<T>(spmv_variant<T>(A) & ~2097152) != nullptr;
+}
+// SpMV workgroups of the pushing interior launch over `count` slices: the
+// interior launch's resident grid less the push workgroups (all resident)
+template <typename T> int Launch<T>::slice_grid_push(const CsrDev &A, int count, int wg0) {
+  const int g = slice_grid(A, count);
+  const int r = spmv_dot_resident<T>(spmv_variant<T>(A) & ~2097152);
+  const int cap = r > 0 ? r - wg0 : g;
+  return std::max(1, std::min(g, cap));
+}
+template <typename T>
+hipError_t Launch<T>::spmv_dot_slices_push(const CsrDev &A, const int *list, int count,
+                                           int part_off, const T *p, T *Ap, CgScalars<T> *st,
+                                           int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                           const PeerDev &P, int wg0) {
+  const int v = spmv_variant<T>(A) & ~2097152;
+  const void *k = spmv_push_kernel<T>(v);
+  if (!k || count < 1 || wg0 % 8) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.sorder = list;
+  a.nsl = count;
+  a.part_off = part_off;
+  a.rev = rev;
+  a.wg0 = wg0;
+  const T *val = (const T *)A.val;
+  PeerDev pd = P;
+  void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
+                   (void *)&ws, (void *)&pd};
+  return hipLaunchKernel(k, dim3(wg0 + slice_grid_push(A, count, wg0)), dim3(kBlock), kargs, 0,
+                         s);
+}
+
 template <typename T>
 hipError_t Launch<T>::flush_group(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                   hipStream_t s, int rev) {
@@ -3252,13 +3442,25 @@ hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int
 }
 template <typename T>
 hipError_t Launch<T>::update_xp(int64_t n, T *x, T *p, const T *r, CgScalars<T> *st,
-                                int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev) {
+                                int slot, RedWs<T> *ws, int np_rr, hipStream_t s, int rev,
+                                const PeerDev *peer) {
+  if (peer)
+    CGX_LAUNCH(k_update_xp_peer<T>, grid_elems(n, kGridUpdateP), n, x, p, r, st, slot, ws, np_rr,
+               rev, *peer);
   CGX_LAUNCH(k_update_xp<T>, grid_elems(n, kGridUpdateP), n, x, p, r, st, slot, ws, np_rr, rev);
 }
 template <typename T>
 hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *const P[4],
                                      const T *r, CgScalars<T> *st, int slot, RedWs<T> *ws,
-                                     int np_rr, hipStream_t s, int rev) {
+                                     int np_rr, hipStream_t s, int rev, const PeerDev *peer) {
+  if (peer && slot == 3)
+    CGX_LAUNCH((k_update_p_defer_peer<T, true>), grid_elems(n, kGridUpdateP), n, x, p, pn,
+               (const T *)P[0], (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev,
+               *peer);
+  if (peer)
+    CGX_LAUNCH((k_update_p_defer_peer<T, false>), grid_elems(n, kGridUpdateP), n, x, p, pn,
+               (const T *)P[0], (const T *)P[1], (const T *)P[2], r, st, slot, ws, np_rr, rev,
+               *peer);
   if (slot == 3) {
     CGX_LAUNCH((k_update_p_defer<T, true>), grid_elems(n, kGridUpdateP), n, x, p, pn,
                (const T *)P[0],

@@ -62,6 +62,11 @@ struct PeerState {            // device, per matrix
   unsigned long long ar;      // all-reduces completed (the tag of the last)
   int fault;                  // a spin timed out: every later peer kernel returns
   int pad;
+  // the tag base of the body in slot s is arb[s & 1]: its push and wait use
+  // it, its two all-reduces base + 1 and base + 2; the second writes
+  // arb[(s + 1) & 1] (read by no kernel of this body, so the all-reduce can
+  // run inside a many-workgroup consumer kernel)
+  unsigned long long arb[2];
 };
 struct PeerDev {  // kernel argument (by value)
   char *ctl[kPeerMax];            // rank q's mailbox + flags, as mapped here
@@ -214,7 +219,8 @@ template <typename T> int peer_push(cgx_csr *A, const T *v_ext, CgScalars<T> *st
 template <typename T> int peer_wait(cgx_csr *A, T *v_ext, CgScalars<T> *st, int slot,
                                     hipStream_t s);
 // *dst = sum over ranks of (sum of part[0..np)), identical bits on every rank
+// which: 0 setup / init, 1 and 2 the body's p.Ap and r.r (k_peer_allreduce)
 template <typename T> int peer_allreduce(cgx_csr *A, const T *part, int np, T *dst,
-                                         CgScalars<T> *st, int slot, hipStream_t s);
+                                         CgScalars<T> *st, int slot, hipStream_t s, int which);
 int peer_destroy(cgx_csr *A);
 }  // namespace cgx

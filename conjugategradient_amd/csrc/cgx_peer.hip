@@ -46,37 +46,18 @@
 #include <vector>
 
 #include "cgx_objects.h"
+#include "cgx_peer_dev.h"
 
 namespace cgx {
 namespace {
 
-__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys(unsigned long long *p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ double ld_sysd(const double *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sysd(double *p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+using peerdev::ld_sys;
+using peerdev::ld_sysd;
+using peerdev::st_sys;
+using peerdev::st_sysd;
+using peerdev::skip_body;
 
-// poll *p >= want; false after `ticks` of the constant wall clock
-__device__ bool spin_ge(const unsigned long long *p, unsigned long long want, long long ticks) {
-  const long long t0 = wall_clock64();
-  while (ld_sys(p) < want) {
-    if (wall_clock64() - t0 > ticks) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return true;
-}
-
-template <typename T> __device__ __forceinline__ bool skip_body(const CgScalars<T> *st, int slot,
-                                                                const PeerState *ps) {
-  return (st && !st->active[slot]) || ps->fault;
-}
+using peerdev::spin_ge;
 
 template <typename T> __device__ void raise_fault(CgScalars<T> *st, int slot, PeerState *ps) {
   ps->fault = 1;
@@ -86,31 +67,13 @@ template <typename T> __device__ void raise_fault(CgScalars<T> *st, int slot, Pe
   }
 }
 
-// k_peer_push: grid = nsend x kPushWG; workgroup (i, g) sends chunk g of
-// neighbour i's send list into its landing buffer, then raises flag
-// [my rank][g] there with the tag of this body (PeerState::ar)
+// k_peer_push: grid = nsend x kPushWG (peerdev::push_wg); the split SpMV
+// of a SELL matrix carries the same workgroups at the front of its interior
+// launch instead (k_spmv_dot_push)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_peer_push(const T *__restrict__ v, PeerDev P,
                                                        CgScalars<T> *st, int slot) {
-  if (skip_body(st, slot, P.state)) return;
-  const unsigned long long tag = P.state->ar;
-  const int i = blockIdx.x / kPushWG, g = blockIdx.x % kPushWG;
-  const int64_t cnt = P.send_cnt[i], off = P.send_off[i];
-  const int64_t c0 = cnt * g / kPushWG, c1 = cnt * (g + 1) / kPushWG;
-  T *dst = reinterpret_cast<T *>(P.land_remote[i]);
-  const int *idx = P.send_idx + off;
-  for (int64_t k = c0 + threadIdx.x; k < c1; k += kBlock) dst[k] = v[idx[k]];
-  // every storing wave drains its stores, then one lane releases them at
-  // system scope and raises the flag (MI355X guide, "Valid forms"; the asm
-  // wait after the fence guards the compiler hazard noted there)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    auto *flag = reinterpret_cast<unsigned long long *>(P.ctl[P.send_rank[i]] + kPeerFlagOff);
-    st_sys(flag + P.rank * kPushWG + g, tag);
-  }
+  peerdev::push_wg<T>(v, P, st, slot, blockIdx.x);
 }
 
 // k_peer_wait: every workgroup's first wave polls the flags of every rank
@@ -121,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_wait(T *__restrict__ v, PeerDev
                                                        CgScalars<T> *st, int slot) {
   __shared__ int ok_s;
   if (skip_body(st, slot, P.state)) return;
-  const unsigned long long tag = P.state->ar;
+  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
   if (threadIdx.x < 64) {
     const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
     bool ok = true;
@@ -144,11 +107,14 @@ __global__ __launch_bounds__(kBlock) void k_peer_wait(T *__restrict__ v, PeerDev
 }
 
 // k_peer_allreduce: one workgroup. *dst = sum over ranks in rank order of
-// each rank's sum of its part[0..np) (fixed order within the rank)
+// each rank's sum of its part[0..np) (fixed order within the rank). which:
+// 0 a setup / init all-reduce (tag ar + 1; both body bases follow it), 1 / 2
+// the body's first / second (tag arb[slot & 1] + which; the second sets the
+// next body's base)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_peer_allreduce(const T *__restrict__ part, int np,
                                                             T *dst, CgScalars<T> *st, int slot,
-                                                            PeerDev P) {
+                                                            PeerDev P, int which) {
   __shared__ double red[kBlock / 64];
   __shared__ int ok_s;
   if (skip_body(st, slot, P.state)) return;
@@ -158,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_allreduce(const T *__restrict__
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   const double mine = ((red[0] + red[1]) + red[2]) + red[3];
-  const unsigned long long tag = P.state->ar + 1;
+  const unsigned long long tag = which ? P.state->arb[slot & 1] + which : P.state->ar + 1;
   const int par = (int)(tag & 1);
   if (threadIdx.x < 64) {
     bool ok = true;
@@ -187,6 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_allreduce(const T *__restrict__
   for (int q = 0; q < P.world; ++q) s += ld_sysd(vals + q);
   *dst = (T)s;
   P.state->ar = tag;
+  if (which == 0) P.state->arb[0] = P.state->arb[1] = tag;
+  if (which == 2) P.state->arb[(slot + 1) & 1] = tag;
 }
 
 constexpr int kWaitGridMax = 256;
@@ -219,9 +187,9 @@ template <typename T> int peer_wait(cgx_csr *A, T *v_ext, CgScalars<T> *st, int 
 
 template <typename T>
 int peer_allreduce(cgx_csr *A, const T *part, int np, T *dst, CgScalars<T> *st, int slot,
-                   hipStream_t s) {
+                   hipStream_t s, int which) {
   hipLaunchKernelGGL(k_peer_allreduce<T>, dim3(1), dim3(kBlock), 0, s, part, np, dst, st, slot,
-                     A->peer.dev);
+                     A->peer.dev, which);
   CGX_HIP(hipGetLastError());
   return CGX_OK;
 }
@@ -231,9 +199,9 @@ template int peer_push<float>(cgx_csr *, const float *, CgScalars<float> *, int,
 template int peer_wait<double>(cgx_csr *, double *, CgScalars<double> *, int, hipStream_t);
 template int peer_wait<float>(cgx_csr *, float *, CgScalars<float> *, int, hipStream_t);
 template int peer_allreduce<double>(cgx_csr *, const double *, int, double *, CgScalars<double> *,
-                                    int, hipStream_t);
+                                    int, hipStream_t, int);
 template int peer_allreduce<float>(cgx_csr *, const float *, int, float *, CgScalars<float> *,
-                                   int, hipStream_t);
+                                   int, hipStream_t, int);
 
 int peer_destroy(cgx_csr *A) {
   Peer &pr = A->peer;
@@ -301,7 +269,7 @@ template <typename T> int self_test(cgx_csr *A, bool *ok) {
     for (int q = 0; q < ctx->world; ++q) want[r] += (T)(q + 1) * (T)(r + 1) + (T)0.5;
     e = hipMemcpyAsync(part, mine, 2 * sizeof(T), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) rc = hip_fail(e, "peer self-test (copy)");
-    if (!rc) rc = peer_allreduce<T>(A, part, 2, res + r, nullptr, 0, s);
+    if (!rc) rc = peer_allreduce<T>(A, part, 2, res + r, nullptr, 0, s, 0);
     if (!rc) {
       e = hipStreamSynchronize(s);  // `part` is reused
       if (e != hipSuccess) rc = hip_fail(e, "peer self-test (all-reduce)");
@@ -390,7 +358,7 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
   if (e == hipSuccess) e = hipMalloc(&pr.state, sizeof(PeerState));
   if (e == hipSuccess) e = hipMemsetAsync(pr.ctl, 0, kPeerCtlBytes, s);
   if (e == hipSuccess) e = hipMemsetAsync(pr.land, 0, std::max<size_t>(1, (size_t)h.n_ghost) * es, s);
-  PeerState st0{1, 0, 0};  // tags start at 1: a zeroed flag never matches
+  PeerState st0{1, 0, 0, {1, 1}};  // tags start at 1: a zeroed flag never matches
   if (e == hipSuccess) e = hipMemcpyAsync(pr.state, &st0, sizeof(st0), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&card.ctl, pr.ctl);
