@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""One GPU running the per-rank slab of the strong-scaling configs on its
+own: 256 x 256 x 32 (256^3 over 8 GPUs) and 512 x 512 x 64 (512^3 over 8),
+the same iteration as bench.py (auto mode, graph replay), no halo and no
+all-reduce. Its time per body is the floor of an 8-GPU body: the work each
+GPU does plus the launch boundaries, without the transport.
+
+    python tools/slab_bench.py
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import conjugategradient_amd as cga  # noqa: E402
+from conjugategradient_amd._native import F64, check, lib  # noqa: E402
+
+
+def main():
+    L = lib()
+    q = cga.Queue(0)
+    for nx, ny, nz, steps in ((256, 256, 32, 2000), (512, 512, 64, 400)):
+        A = cga.Matrix.poisson(q, 3, nx, ny, nz)
+        n = A.N()
+        sched = A.schedule()
+        b = cga.DeviceArray(q, n, np.float64)
+        x = cga.DeviceArray(q, n, np.float64)
+        check(L.cgx_iota(q.handle, F64, b.ptr, n, 0.0))
+        x.fill(0.0)
+        cg = C.c_void_p()
+        check(L.cgx_cg_create(q.handle, sched, C.byref(cg)))
+        check(L.cgx_cg_config(cg, 64, 1))
+        mode, v = C.c_int(), C.c_int()
+        check(L.cgx_cg_get_mode(cg, C.byref(mode)))
+        check(L.cgx_csr_variant(sched, C.byref(v)))
+        check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 20 + steps + 1))
+        tot, st = C.c_int64(), C.c_int()
+        check(L.cgx_cg_run(cg, 20, C.byref(tot), C.byref(st)))
+        check(L.cgx_sync(q.handle))
+        t = time.perf_counter()
+        check(L.cgx_cg_run(cg, steps, C.byref(tot), C.byref(st)))
+        check(L.cgx_sync(q.handle))
+        dt = time.perf_counter() - t
+        print(json.dumps({"slab": [nx, ny, nz], "rows": n, "mode": mode.value,
+                          "spmv_variant": v.value, "bodies": steps,
+                          "us_per_body": round(dt / steps * 1e6, 2),
+                          "it_per_s": round(steps / dt, 1)}), flush=True)
+        L.cgx_cg_destroy(cg)
+        del A, b, x
+
+
+if __name__ == "__main__":
+    main()
