@@ -49,10 +49,20 @@ def main():
         check(L.cgx_cg_run(cg, steps, C.byref(tot), C.byref(st)))
         check(L.cgx_sync(q.handle))
         dt = time.perf_counter() - t
+        # per-kernel HIP-event pass (eager launches; the durations, not the gaps)
+        avg = (C.c_double * 4)()
+        calls = (C.c_int64 * 4)()
+        check(L.cgx_cg_set_kernel_timing(cg, 1))
+        check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 101))
+        check(L.cgx_cg_run(cg, 100, C.byref(tot), C.byref(st)))
+        check(L.cgx_cg_kernel_times(cg, avg, calls))
         print(json.dumps({"slab": [nx, ny, nz], "rows": n, "mode": mode.value,
                           "spmv_variant": v.value, "bodies": steps,
                           "us_per_body": round(dt / steps * 1e6, 2),
-                          "it_per_s": round(steps / dt, 1)}), flush=True)
+                          "it_per_s": round(steps / dt, 1),
+                          "kernel_us": {"spmv": round(avg[1] * 1e3, 2),
+                                        "update_r": round(avg[2] * 1e3, 2),
+                                        "p_update": round(avg[3] * 1e3, 2)}}), flush=True)
         L.cgx_cg_destroy(cg)
         del A, b, x
 
