@@ -54,6 +54,15 @@ def test_byte_accounting():
     # r update 24 n; x/p update 40 n (mode 1) or 34 n averaged (mode 3)
     assert bench.update_bytes_per_iter(n, 1) == 64 * n
     assert bench.update_bytes_per_iter(n, 3) == 58 * n
+    # mode 4: the p update lives in the SpMV (r, p_{k-1} read, p_k, Ap
+    # written: 32 n beside the matrix stream); r update 24 n, x flush 12 n
+    assert bench.update_bytes_per_iter(n, 4) == 36 * n
+    assert bench.spmv_bytes_per_iter(1000, n, 4) == 1000 + 32 * n
+    assert bench.spmv_bytes_per_iter(1000, n, 3) == 1000 + 16 * n
+    # per iteration: mode 4 moves 6 n less than mode 3 (68 n against 74 n)
+    m3 = bench.spmv_bytes_per_iter(0, n, 3) + bench.update_bytes_per_iter(n, 3)
+    m4 = bench.spmv_bytes_per_iter(0, n, 4) + bench.update_bytes_per_iter(n, 4)
+    assert (m3, m4) == (74 * n, 68 * n)
 
 
 def test_job_cores_reports_host():
