@@ -177,6 +177,16 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
       return !e || std::atoi(e) != 0;
     }();
     const bool merged = split && wg0 > 0 && merge_on && Launch<T>::push_supported(A->dev);
+    // $CGX_PEER_WAIT_FOLD=1: the boundary launch carries the wait in its
+    // first kWaitWG workgroups (k_spmv_dot_wait), one launch less. Off by
+    // default: on the one-GPU rehearsal its spinning workgroups cost more
+    // than the launch (2,595-2,618 against 2,714 it/s, profiles/
+    // r02_waitfold_bench2.log); a node with one rank per GPU may differ
+    static const bool fold_on = [] {
+      const char *e = std::getenv("CGX_PEER_WAIT_FOLD");
+      return e && std::atoi(e) != 0;
+    }();
+    const bool folded = merged && fold_on && A->split_nb > 0;
     if (!merged && (rc = peer_push<T>(A, p, st, slot, s))) return rc;
     const int gi = !split ? 0
                    : merged ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
@@ -189,6 +199,9 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
+           if (e == hipSuccess && folded)
+             return Launch<T>::spmv_dot_slices_wait(A->dev, A->d_split + A->split_ni, A->split_nb,
+                                                    gi, p, Ap, st, slot, ws, s, rev, A->peer.dev);
            if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
            if (e == hipSuccess)
              e = split ? Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,
@@ -197,7 +210,9 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            return e;
          })))
       return rc;
-    *np = split ? gi + Launch<T>::slice_grid(A->dev, A->split_nb) : Launch<T>::spmv_parts(A->dev);
+    *np = !split   ? Launch<T>::spmv_parts(A->dev)
+          : folded ? gi + Launch<T>::slice_grid_push(A->dev, A->split_nb, kWaitWG)
+                   : gi + Launch<T>::slice_grid(A->dev, A->split_nb);
     return CGX_OK;
   }
   if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192))) {

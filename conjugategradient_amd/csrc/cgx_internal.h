@@ -185,6 +185,11 @@ template <typename T> struct Launch {
                                          int part_off, const T *p, T *Ap, CgScalars<T> *st,
                                          int slot, RedWs<T> *ws, hipStream_t s, int rev,
                                          const PeerDev &P, int wg0);
+  // the boundary slices with the halo wait in the launch's first kWaitWG
+  // workgroups (k_spmv_dot_wait); its SpMV workgroups: slice_grid_push(.., kWaitWG)
+  static hipError_t spmv_dot_slices_wait(const CsrDev &A, const int *list, int count,
+                                         int part_off, T *p, T *Ap, CgScalars<T> *st, int slot,
+                                         RedWs<T> *ws, hipStream_t s, int rev, const PeerDev &P);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);

@@ -58,6 +58,7 @@ struct Halo {
 // a partitioned iteration is all kernels and graph-capturable.
 constexpr int kPeerMax = 16;  // ranks of one node
 constexpr int kPushWG = 16;   // push workgroups (and flags) per neighbour
+constexpr int kWaitWG = 8;    // halo wait workgroups leading the boundary SpMV launch
 struct PeerState {            // device, per matrix
   unsigned long long ar;      // all-reduces completed (the tag of the last)
   int fault;                  // a spin timed out: every later peer kernel returns
@@ -67,6 +68,9 @@ struct PeerState {            // device, per matrix
   // arb[(s + 1) & 1] (read by no kernel of this body, so the all-reduce can
   // run inside a many-workgroup consumer kernel)
   unsigned long long arb[2];
+  // k_spmv_dot_wait: wait workgroup w raises ready[w] to the body's tag once
+  // its share of the ghosts is in place; the boundary slices wait for all
+  unsigned long long ready[kWaitWG];
 };
 struct PeerDev {  // kernel argument (by value)
   char *ctl[kPeerMax];            // rank q's mailbox + flags, as mapped here

@@ -59,13 +59,7 @@ using peerdev::skip_body;
 
 using peerdev::spin_ge;
 
-template <typename T> __device__ void raise_fault(CgScalars<T> *st, int slot, PeerState *ps) {
-  ps->fault = 1;
-  if (st) {
-    st->active[slot] = 0;  // the rest of the body returns; the p update
-    st->stopped = 3;       // then clears the next slot (k_update_p_defer)
-  }
-}
+using peerdev::raise_fault;
 
 // k_peer_push: grid = nsend x kPushWG (peerdev::push_wg); the split SpMV
 // of a SELL matrix carries the same workgroups at the front of its interior
@@ -358,7 +352,7 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
   if (e == hipSuccess) e = hipMalloc(&pr.state, sizeof(PeerState));
   if (e == hipSuccess) e = hipMemsetAsync(pr.ctl, 0, kPeerCtlBytes, s);
   if (e == hipSuccess) e = hipMemsetAsync(pr.land, 0, std::max<size_t>(1, (size_t)h.n_ghost) * es, s);
-  PeerState st0{1, 0, 0, {1, 1}};  // tags start at 1: a zeroed flag never matches
+  PeerState st0{1, 0, 0, {1, 1}, {}};  // tags start at 1: a zeroed flag never matches
   if (e == hipSuccess) e = hipMemcpyAsync(pr.state, &st0, sizeof(st0), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&card.ctl, pr.ctl);

@@ -64,6 +64,16 @@ def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
     assert r["peer"] == [int(transport.endswith("-peer"))] * nproc
 
 
+def test_folded_halo_wait(monkeypatch):
+    """$CGX_PEER_WAIT_FOLD=1: the halo wait rides in the boundary SpMV
+    launch's first workgroups (k_spmv_dot_wait), the boundary slices wait on
+    their ready flags; same x as the oracle at 3 ranks."""
+    monkeypatch.setenv("CGX_PEER_WAIT_FOLD", "1")
+    r = _run(3, "host-peer", 20, 3)
+    assert r["ok"], r
+    assert r["peer"] == [1, 1, 1]
+
+
 @pytest.mark.parametrize("nproc,grid,mode", [(2, 24, 0), (3, 20, 3)])
 def test_async_host_halo_matches_synchronous(nproc, grid, mode):
     """The overlapped halo ordering of the RCCL branch (cgx_dist.cpp

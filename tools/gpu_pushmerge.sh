@@ -14,9 +14,10 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 500
     > $O/pytest_dist.log 2>&1 || { echo "pytest failed: $?"; tail -40 $O/pytest_dist.log; exit 1; }
 tail -1 $O/pytest_dist.log
 for rep in 1 2; do
-for m in 1 0; do
-  CGX_PEER_AR_FUSE=$m CGX_PEER_PUSH_MERGE=$m timeout -k 10 240 python -u bench.py --gpus 2 --transport host-peer --no-cpu --no-general --steps 300 --profile-steps 0 > $O/bench2_m${m}_$rep.log 2>&1 || { echo "bench2 m$m failed"; tail -20 $O/bench2_m${m}_$rep.log; exit 1; }
-  grep '^{' $O/bench2_m${m}_$rep.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('merge', $m, d['n_gpus'], d['iterations_per_s'], d['config']['transport'])"
+for cfg in "1 1" "1 0" "0 0"; do
+  set -- $cfg
+  CGX_PEER_AR_FUSE=$1 CGX_PEER_PUSH_MERGE=$1 CGX_PEER_WAIT_FOLD=$2 timeout -k 10 240 python -u bench.py --gpus 2 --transport host-peer --no-cpu --no-general --steps 300 --profile-steps 0 > $O/bench2_m$1_f$2_$rep.log 2>&1 || { echo "bench2 $cfg failed"; tail -20 $O/bench2_m$1_f$2_$rep.log; exit 1; }
+  grep '^{' $O/bench2_m$1_f$2_$rep.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('merge+fuse', '$1', 'fold', '$2', d['n_gpus'], d['iterations_per_s'])"
 done
 done
 timeout -k 10 240 python -u bench.py --no-cpu --no-general --steps 300 > $O/bench1.log 2>&1 || { echo "bench1 failed"; tail -20 $O/bench1.log; exit 1; }
