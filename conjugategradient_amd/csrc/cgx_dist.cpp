@@ -283,6 +283,9 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
 }
 
 int dist_destroy_halo(cgx_csr *A) {
+  // an exchange still queued on the comm stream reads this matrix's halo
+  // (the asynchronous host transport's host function): drain it first
+  if (A->ctx && A->ctx->cstream) (void)hipStreamSynchronize(A->ctx->cstream);
   if (A->ev_pack) (void)hipEventDestroy(A->ev_pack);
   if (A->ev_halo) (void)hipEventDestroy(A->ev_halo);
   A->ev_pack = A->ev_halo = nullptr;
