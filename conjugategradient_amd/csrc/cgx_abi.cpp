@@ -1506,7 +1506,10 @@ int autotune_spmv(cgx_csr *A) {
   // against 281 with default-policy loads, a choice the isolated timing below
   // cannot see (it ran both within 1%). Such matrices tune the format only.
   const bool big = bytes > (int64_t(512) << 20);
-  std::vector<int> cands = big ? std::vector<int>{15} : std::vector<int>{13, 15};
+  // cache-resident CSR also tries the unpipelined paired loop (5) and the
+  // quad loads (265): the G3 stand-in's SpMV runs 23.6 / 23.8 us in them
+  // against 25.3 in the pipelined 13 (profiles/r02_irr_variants.log)
+  std::vector<int> cands = big ? std::vector<int>{15} : std::vector<int>{13, 15, 5, 265};
   if (A->dev.sl) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
