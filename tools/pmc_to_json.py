@@ -40,7 +40,7 @@ out = {
                f"(tools/gpu_final.sh, run {tag}), mean over {nf}/{nw} dispatches of {kern}; "
                "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B, "
                "MI355X_MICROARCH.md HBM/rocprofv3 section); KB = 1024 B"),
-    "raw": f"profiles/r02h_pmc_fetch.txt, profiles/r02h_pmc_write.txt" if tag == "r2h" else f"profiles/{tag}_pmc_spmv.txt",
+    "raw": f"profiles/r02{tag[2:]}_pmc_fetch.txt, profiles/r02{tag[2:]}_pmc_write.txt" if tag.startswith("r2") else f"profiles/{tag}_pmc_spmv.txt",
     "algorithmic_bytes_per_launch": 12 * nnz + 4 * (n + 1) + 16 * n,
     "note": ("SELL-P copy with value codes: per row pair and chunk of 8 slots one 8-byte "
              "word of 4-bit codes into the matrix's value dictionary (2 values at 256^3), "
