@@ -5,7 +5,7 @@ the same iteration as bench.py (auto mode, graph replay), no halo and no
 all-reduce. Its time per body is the floor of an 8-GPU body: the work each
 GPU does plus the launch boundaries, without the transport.
 
-    python tools/slab_bench.py
+    python tools/slab_bench.py [dim,nx,ny,nz,bodies ...]
 """
 from __future__ import annotations
 
@@ -27,8 +27,11 @@ from conjugategradient_amd._native import F64, check, lib  # noqa: E402
 def main():
     L = lib()
     q = cga.Queue(0)
-    for nx, ny, nz, steps in ((256, 256, 32, 2000), (512, 512, 64, 400)):
-        A = cga.Matrix.poisson(q, 3, nx, ny, nz)
+    shapes = ((3, 256, 256, 32, 2000), (3, 512, 512, 64, 400))
+    if len(sys.argv) > 1:  # e.g. 2,4096,4096,1,400
+        shapes = tuple(tuple(int(v) for v in a.split(",")) for a in sys.argv[1:])
+    for dim, nx, ny, nz, steps in shapes:
+        A = cga.Matrix.poisson(q, dim, nx, ny, nz)
         n = A.N()
         sched = A.schedule()
         b = cga.DeviceArray(q, n, np.float64)
@@ -56,13 +59,14 @@ def main():
         check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 101))
         check(L.cgx_cg_run(cg, 100, C.byref(tot), C.byref(st)))
         check(L.cgx_cg_kernel_times(cg, avg, calls))
-        print(json.dumps({"slab": [nx, ny, nz], "rows": n, "mode": mode.value,
+        print(json.dumps({"slab": [nx, ny, nz], "dim": dim, "rows": n, "mode": mode.value,
                           "spmv_variant": v.value, "bodies": steps,
                           "us_per_body": round(dt / steps * 1e6, 2),
                           "it_per_s": round(steps / dt, 1),
                           "kernel_us": {"spmv": round(avg[1] * 1e3, 2),
                                         "update_r": round(avg[2] * 1e3, 2),
-                                        "p_update": round(avg[3] * 1e3, 2)}}), flush=True)
+                                        "p_update_or_flush": round(avg[3] * 1e3, 2)}}),
+              flush=True)
         L.cgx_cg_destroy(cg)
         del A, b, x
 
