@@ -2,6 +2,8 @@
 # grid caps of the vector kernels for vectors under 8 M elements (the G3
 # stand-in, the 256^3/8 slab): interleaved A/B of CGX_GRID_R_SMALL /
 # CGX_GRID_P_SMALL
+# (the CGX_GRID_*_SMALL knobs existed only in the A/B build of that run; the
+# defaults won and the knobs were removed)
 set -o pipefail
 O=gpurun_out/${1:-smallgrid}
 mkdir -p $O
