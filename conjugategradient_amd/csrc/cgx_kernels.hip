@@ -2857,8 +2857,13 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   const V *Q[3] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
                    reinterpret_cast<const V *>(P2)};
   auto body = [&](int64_t i) {
-    const V pv = p2[i];
-    const V rv = rv2[i];
+    // r and p_k are not re-read before the next SpMV and update_r have
+    // streamed them out of the Infinity Cache: non-temporal loads leave it
+    // to p_{k+1}, which the next SpMV reads first (+2.9% per iteration at
+    // 256^3: SpMV 90.3 against 93.2 us, this kernel 88.4 against 91.3;
+    // profiles/r02_pupd_nt.log)
+    const V pv = ldv<kStreamNt, T>(p2 + i);
+    const V rv = ldv<kStreamNt, T>(rv2 + i);
     V q[3], xv;
     if constexpr (FLUSH) {  // x and the old p buffers: not read again soon
       xv = ldv<kStreamNt, T>(x2 + i);
