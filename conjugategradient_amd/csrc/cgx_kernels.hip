@@ -378,14 +378,17 @@ template <typename T> struct GatherX {
     return ((const __attribute__((address_space(4))) T *)x)[i];
   }
 };
-template <typename T> struct GatherP {
+// NTP: p_{k-1} read non-temporally (the plane march reads each of its lines
+// once as a center; mode 4 reads it again only in the slot-3 x flush)
+template <typename T, bool NTP = false> struct GatherP {
   const T *__restrict__ r;
   const T *__restrict__ pp;
   T beta;
   __device__ __forceinline__ T operator()(int c) const { return r[c] + beta * pp[c]; }
   __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
     using U = typename PairU<T>::V;
-    const U a = *reinterpret_cast<const U *>(r + c), b = *reinterpret_cast<const U *>(pp + c);
+    const U a = *reinterpret_cast<const U *>(r + c);
+    const U b = ldg<NTP>(reinterpret_cast<const U *>(pp + c));
     U o;
     o.x = a.x + beta * b.x;
     o.y = a.y + beta * b.y;
@@ -1954,10 +1957,10 @@ template <typename T> struct EpiFused {
 // reads it (GatherP, also for the center pair the value-code forms hand to
 // pre2c) and stored once into this body's p buffer; then helper = A p_k and
 // value2 += helper.p_k (CG.hpp:374-379) exactly as EpiDot.
-template <typename T> struct EpiFD {
+template <typename T, bool NTP = false> struct EpiFD {
   T *__restrict__ Ap;
   T *__restrict__ pc;
-  GatherP<T> g;
+  GatherP<T, NTP> g;
   T acc, pv, pv1;
   __device__ __forceinline__ void pre(int i) { pv = g(i); }
   __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
@@ -2173,8 +2176,9 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd(
       st->rxr[slot] = rr;
     }
   }
-  const GatherP<T> g{r, pold, beta};
-  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  constexpr bool NTP = (V & 2097152) != 0;  // plane march: p_{k-1} lines read once
+  const GatherP<T, NTP> g{r, pold, beta};
+  EpiFD<T, NTP> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, g, e, sm);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
