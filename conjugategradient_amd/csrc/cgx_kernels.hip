@@ -128,6 +128,18 @@ __device__ __forceinline__ void parts_load(const T *__restrict__ part, int np,
   for (int k = 0; k < kPartsPerThread; ++k)  // unconditional (np >= 1): exact vmcnt waits
     pl[k] = part[min((int)threadIdx.x + k * kBlock, np - 1)];
 }
+// parts_load for a kernel with no stream loads behind it: only the np
+// partials are loaded (a few at small grids; parts_load issues
+// kPartsPerThread per thread whatever np is)
+template <typename T>
+__device__ __forceinline__ void parts_load_np(const T *__restrict__ part, int np,
+                                              T (&pl)[kPartsPerThread]) {
+#pragma unroll
+  for (int k = 0; k < kPartsPerThread; ++k) {
+    const int i = (int)threadIdx.x + k * kBlock;
+    pl[k] = i < np ? part[i] : T(0);
+  }
+}
 template <typename T>
 __device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T *lds) {
   __shared__ T bc;
@@ -142,6 +154,29 @@ __device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T
   if (threadIdx.x == 0) bc = ((lds[0] + lds[1]) + lds[2]) + lds[3];
   lds_barrier();
   return bc;
+}
+
+// Late active check (CGX_LATE_ACTIVE, default on; A/B builds -DCGX_LATE_ACTIVE=0):
+// a body kernel issues its first loads (scalars, partials, first stream
+// block; valid memory whether or not the body runs) together with the
+// active flag and branches on the flag afterwards, so a cache-resident
+// body pays one load round trip before its first store instead of two.
+// LLVM sinks a load whose only uses lie in one successor of the branch;
+// keep() in the inactive successor uses them there too (an empty asm: it
+// waits for them on that path only), so they stay where they were issued.
+#ifndef CGX_LATE_ACTIVE
+#define CGX_LATE_ACTIVE 1
+#endif
+template <typename T> __device__ __forceinline__ void keep(const T &a) {
+  if constexpr (sizeof(T) == 16) {
+    asm volatile("" ::"v"(a.x), "v"(a.y));
+  } else {
+    asm volatile("" ::"v"(a));
+  }
+}
+template <typename T, int K> __device__ __forceinline__ void keep(const T (&a)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) keep(a[k]);
 }
 
 // Grid-wide deterministic reduction. Every workgroup publishes its block sum
@@ -388,7 +423,10 @@ template <typename T, bool NTP = false> struct GatherP {
   __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
     using U = typename PairU<T>::V;
     const U a = *reinterpret_cast<const U *>(r + c);
-    const U b = ldg<NTP>(reinterpret_cast<const U *>(pp + c));
+    const U *pb = reinterpret_cast<const U *>(pp + c);
+    U b;
+    if constexpr (NTP) b = __builtin_nontemporal_load(pb);
+    else b = *pb;
     U o;
     o.x = a.x + beta * b.x;
     o.y = a.y + beta * b.y;
@@ -2153,6 +2191,8 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd(
     int np_rr) {
   __shared__ LdsOf<T, V> sm;
   const int prev = (slot + 3) & 3;
+  // (the flag checked before the partials' loads: CGX_LATE_ACTIVE's form was
+  // 0.16 us slower here at 128^2, profiles/r02_late_active.log)
   const long long bodies = st->bodies;
   const bool act = st->active[slot] != 0;
   if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
@@ -2298,10 +2338,15 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // rule (mode 4, kernel 2 of 2): this kernel also runs the stop rule
   // (CG.hpp:396-404, 436: on the r.r the body started with, which k_spmv_fd
   // recorded) and marks the body's x update pending (ran[slot])
+  const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
+#if CGX_LATE_ACTIVE
+  const bool act = cst->active[slot] != 0;  // branched on after the first loads
+#else
   if (!st->active[slot]) {
     if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
     return;
   }
+#endif
   __shared__ T red[4];
   __shared__ int flag;
   using V = typename Vec2<T>::V;
@@ -2318,7 +2363,6 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // alpha), then the partials are summed while that block is in flight.
   // scalar loads (lgkmcnt): a vector load issued after the prefetch would
   // make its wait drain the prefetch too
-  const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
   const T rxr = cst->rxr[slot];
   const T pAp_st = cst->pAp[slot];
   T pl[kPartsPerThread];
@@ -2331,6 +2375,17 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     rv[u] = ri2[j];
     av[u] = ldv<kStreamNt, T>(a2 + j);  // Ap is dead after this kernel
   }
+#if CGX_LATE_ACTIVE
+  if (!act) {
+    keep(rxr);
+    keep(pAp_st);
+    if (from_parts) keep(pl);
+    keep(rv);
+    keep(av);
+    if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
+    return;
+  }
+#endif
   T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
   if constexpr (PEER) {
     __shared__ double wres;
@@ -2822,6 +2877,24 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
                                                     CgScalars<T> *st, int slot, RedWs<T> *ws,
                                                     int np_rr, int rev, const PeerDev *PD) {
   const int nxt = (slot + 1) & 3;
+#if CGX_LATE_ACTIVE
+  // the flag, rxr and the r.r partials in one round trip
+  const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
+  const bool act = cst->active[slot] != 0;
+  const T rxr = cst->rxr[slot];
+  const T rr_st = cst->rr[slot];
+  T pl[kPartsPerThread];
+  if (np_rr > 0) parts_load_np(ws->rr_part, np_rr, pl);
+  if (!act) {
+    keep(rxr);
+    keep(rr_st);
+    if (np_rr > 0) keep(pl);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
+    return;
+  }
+  __shared__ T red[4];
+  T rr = np_rr > 0 ? parts_sum(pl, np_rr, red) : rr_st;
+#else
   if (!st->active[slot]) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
@@ -2829,6 +2902,7 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   __shared__ T red[4];
   const T rxr = st->rxr[slot];
   T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+#endif
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
