@@ -10,9 +10,11 @@ Poisson CSR (fp64 values, int32 indices, b_i = i + 1, x0 = 0).
 * N = 1: the 256^3 grid (the metric's headline config) on one GPU.
 * N > 1: strong scaling by default — the same global grid (256^3; --grid 512
   is BASELINE config 4) split into contiguous z-slabs, one rank per GPU;
-  the halo exchange of p and the two dot all-reduces run over xGMI (device
-  peer transport where it passes its self-test, else RCCL). --weak gives
-  every rank its own 256^3 slab instead.
+  the halo exchange of p and the two dot all-reduces run over xGMI: the
+  device peer transport when it first solved a small slab problem on this
+  node to the RCCL transport's answer (validate_peer: accuracy, body count,
+  x to 1e-10; reported as config.transport_validation), else RCCL. --weak
+  gives every rank its own 256^3 slab instead.
 * `python bench.py --gpus N` with no launcher environment starts its own N
   ranks (torch.distributed.run, 127.0.0.1) as a child process before touching
   any GPU; under a launcher, WORLD_SIZE must equal --gpus.
@@ -114,8 +116,9 @@ def parse(argv=None):
                          "4 two kernels (p update folded into the SpMV), x deferred")
     ap.add_argument("--transport", choices=["auto", "rccl", "peer", "host", "host-peer"],
                     default="auto",
-                    help="N>1 collectives: auto (device peer transport over xGMI when its "
-                         "self-test passes, else RCCL), rccl, peer (fail if unavailable), "
+                    help="N>1 collectives: auto (device peer transport over xGMI when it "
+                         "solves a validation problem to RCCL's answer on this node, else "
+                         "RCCL), rccl, peer (fail if unavailable), "
                          "host (host-staged test transport: lets ranks share one GPU; "
                          "rehearsal only, numbers meaningless), host-peer (host setup, "
                          "device peer iteration: a one-GPU rehearsal of the peer path)")
@@ -300,9 +303,23 @@ def run(args) -> None:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
                                None, C.byref(A)))
     peer_note = None
-    if world > 1 and args.transport in ("auto", "peer", "host-peer"):
-        # device peer transport over xGMI: verified by a self-test on every
-        # rank; all ranks agree on the outcome (else the setup transport stays)
+    validation = None
+    use_peer = world > 1 and args.transport in ("peer", "host-peer")
+    if world > 1 and args.transport in ("auto", "host-peer"):
+        # the device peer transport is used only after it solved a small slab
+        # problem on THIS node to the same answer as the setup transport
+        # (validate_peer; RCCL, or the host transport of the one-GPU
+        # rehearsal); otherwise the numbers come from the setup transport
+        validation = validate_peer(L, q, world, rank, dist)
+        use_peer = validation["ok"]
+        if not use_peer and args.transport == "host-peer":
+            raise SystemExit(f"bench.py: peer transport failed its validation: "
+                             f"{validation.get('why')}")
+        if not use_peer:
+            peer_note = validation.get("why")
+    if use_peer:
+        # verified by a self-test on every rank; all ranks agree on the
+        # outcome (else the setup transport stays)
         ok = C.c_int(0)
         check(L.cgx_dist_peer_enable(A, C.byref(ok)))
         if ok.value:
@@ -330,15 +347,18 @@ def run(args) -> None:
     if args.warmup:
         check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
 
+    # the graphs the timed run replays are captured here, untimed
+    check(L.cgx_cg_prepare(cg, args.steps))
+
     # ---- timed region ----------------------------------------------------------
+    # the solver's stream is the only one with work (q.wait() drains it; the
+    # run itself returns after its last chunk finished)
+    q.wait()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    q.wait()
     t0 = time.perf_counter()
     check(L.cgx_cg_run(cg, args.steps, C.byref(bodies), C.byref(stopped)))
     q.wait()
-    torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
@@ -449,6 +469,7 @@ def run(args) -> None:
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
                        "peer_fallback_reason": peer_note,
+                       "transport_validation": validation,
                        "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies",
                                      4: "2 kernels (p update in the SpMV), x update deferred "
@@ -465,6 +486,86 @@ def run(args) -> None:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
+    """Solve a small slab problem (nxy x nxy x planes*world, `planes` z-planes
+    per rank, b_i = i + 1, x0 = 0) twice on this node: over the device peer
+    transport and over the context's setup transport (RCCL; the host
+    transport in the one-GPU rehearsal). The peer transport passes when both solves
+    converge (accuracy() < 1e-20), their body counts agree within 2, and
+    their x agree to 1e-10 relative (SURVEY §8(c) tolerances). Collective;
+    every rank returns the same verdict."""
+    import numpy as np
+    import torch
+
+    import conjugategradient_amd as cga
+    from conjugategradient_amd._native import F64, check
+
+    nz = planes * world
+    n_local = nxy * nxy * planes
+    begin = rank * n_local
+    nnz = L.cgx_poisson_nnz(3, nxy, nxy, nz, begin, begin + n_local)
+    rows = cga.DeviceArray(q, n_local + 1, np.int32)
+    cols = cga.DeviceArray(q, nnz, np.int32)
+    vals = cga.DeviceArray(q, nnz, np.float64)
+    check(L.cgx_poisson_fill(q.handle, F64, 3, nxy, nxy, nz, begin, begin + n_local, rows.ptr,
+                             cols.ptr, vals.ptr))
+    b = cga.DeviceArray(q, n_local, np.float64)
+    check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(begin)))
+    out, xs = {}, {}
+    why = None
+    for name in ("peer", "setup"):
+        A = C.c_void_p()
+        check(L.cgx_csr_create_dist(q.handle, n_local * world, begin, n_local, nnz, rows.ptr,
+                                    cols.ptr, vals.ptr, F64, C.byref(A)))
+        try:
+            if name == "peer":
+                ok = C.c_int(0)
+                check(L.cgx_dist_peer_enable(A, C.byref(ok)))
+                if not ok.value:
+                    why = "peer self-test: " + L.cgx_last_error().decode()
+                    out[name] = {"enabled": False}
+                    continue
+            x = cga.DeviceArray(q, n_local, np.float64)
+            x.fill(0.0)
+            cg = C.c_void_p()
+            check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+            bodies, rxr, acc = C.c_int64(), C.c_double(), C.c_double()
+            rc = L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, -1, C.byref(bodies), C.byref(rxr))
+            if rc == 0:
+                check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
+                xs[name] = x.download()
+                out[name] = {"bodies": int(bodies.value), "accuracy": float(acc.value)}
+            else:
+                why = f"{name} solve failed: " + L.cgx_last_error().decode()
+                out[name] = {"error": why}
+            L.cgx_cg_destroy(cg)
+        finally:
+            L.cgx_csr_destroy(A)
+    ok_local = "peer" in xs and "setup" in xs
+    d2 = r2 = 0.0
+    if ok_local:
+        d2 = float(np.sum((xs["peer"] - xs["setup"]) ** 2))
+        r2 = float(np.sum(xs["setup"] ** 2))
+    t = torch.tensor([d2, r2, 0.0 if ok_local else 1.0], dtype=torch.float64)
+    dist.all_reduce(t)
+    rel = math.sqrt(t[0].item() / t[1].item()) if t[1].item() > 0 else float("inf")
+    ok = t[2].item() == 0.0
+    if ok:
+        p, r = out["peer"], out["setup"]
+        ok = (abs(p["bodies"] - r["bodies"]) <= 2 and p["accuracy"] < 1e-20
+              and r["accuracy"] < 1e-20 and rel <= 1e-10)
+        if not ok:
+            why = f"peer and setup-transport solves disagree: {out}, rel {rel:.3e}"
+    # every rank's verdict (accuracy and bodies are global: the same on all)
+    v = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+    dist.all_reduce(v)
+    ok = v.item() == 0.0
+    if not ok and why is None:
+        why = "another rank's validation failed"
+    return {"ok": bool(ok), "grid": [nxy, nxy, nz], "tol": tol, "solves": out,
+            "x_rel_peer_vs_setup": rel, "why": why}
 
 
 def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):

@@ -49,6 +49,7 @@ _SIGS = {
     "cgx_sync": (_i32, [_vp]),
     "cgx_get_stream": (_i32, [_vp, C.POINTER(_vp)]),
     "cgx_get_device": (_i32, [_vp, C.POINTER(_i32)]),
+    "cgx_max_work_group_size": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_alloc": (_i32, [_vp, _sz, C.POINTER(_vp)]),
     "cgx_free": (_i32, [_vp, _vp]),
     "cgx_h2d": (_i32, [_vp, _vp, _vp, _sz]),
@@ -81,6 +82,8 @@ _SIGS = {
     "cgx_cg_solve": (_i32, [_vp, _vp, _vp, _dbl, _i64, C.POINTER(_i64), C.POINTER(_dbl)]),
     "cgx_cg_begin": (_i32, [_vp, _vp, _vp, _dbl, _i64]),
     "cgx_cg_run": (_i32, [_vp, _i64, C.POINTER(_i64), C.POINTER(_i32)]),
+    "cgx_cg_prepare": (_i32, [_vp, _i64]),
+    "cgx_cg_rxr": (_i32, [_vp, C.POINTER(_dbl)]),
     "cgx_cg_set_kernel_timing": (_i32, [_vp, _i32]),
     "cgx_cg_kernel_times": (_i32, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "cgx_cg_config": (_i32, [_vp, _i32, _i32]),

@@ -177,16 +177,10 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
       return !e || std::atoi(e) != 0;
     }();
     const bool merged = split && wg0 > 0 && merge_on && Launch<T>::push_supported(A->dev);
-    // $CGX_PEER_WAIT_FOLD=1: the boundary launch carries the wait in its
-    // first kWaitWG workgroups (k_spmv_dot_wait), one launch less. Off by
-    // default: on the one-GPU rehearsal its spinning workgroups cost more
-    // than the launch (2,595-2,618 against 2,714 it/s, profiles/
-    // r02_waitfold_bench2.log); a node with one rank per GPU may differ
-    static const bool fold_on = [] {
-      const char *e = std::getenv("CGX_PEER_WAIT_FOLD");
-      return e && std::atoi(e) != 0;
-    }();
-    const bool folded = merged && fold_on && A->split_nb > 0;
+    // (the wait stays a launch of its own: round 2's folded form had the
+    // boundary workgroups spin on flags raised by the same launch's first
+    // workgroups, which relies on their being resident; removed in round 3,
+    // DESIGN.md §9)
     if (!merged && (rc = peer_push<T>(A, p, st, slot, s))) return rc;
     const int gi = !split ? 0
                    : merged ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
@@ -199,9 +193,6 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
-           if (e == hipSuccess && folded)
-             return Launch<T>::spmv_dot_slices_wait(A->dev, A->d_split + A->split_ni, A->split_nb,
-                                                    gi, p, Ap, st, slot, ws, s, rev, A->peer.dev);
            if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
            if (e == hipSuccess)
              e = split ? Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,
@@ -210,9 +201,7 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            return e;
          })))
       return rc;
-    *np = !split   ? Launch<T>::spmv_parts(A->dev)
-          : folded ? gi + Launch<T>::slice_grid_push(A->dev, A->split_nb, kWaitWG)
-                   : gi + Launch<T>::slice_grid(A->dev, A->split_nb);
+    *np = !split ? Launch<T>::spmv_parts(A->dev) : gi + Launch<T>::slice_grid(A->dev, A->split_nb);
     return CGX_OK;
   }
   if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192))) {
@@ -450,17 +439,19 @@ int flush_pending_x(cgx_cg *cg) {
 }
 
 void drop_graph(cgx_cg *cg) {
-  if (cg->graph) (void)hipGraphExecDestroy(cg->graph);
-  cg->graph = nullptr;
+  for (auto &kv : cg->graphs) (void)hipGraphExecDestroy(kv.second);
+  cg->graphs.clear();
 }
 
-// Capture `iters` iterations (slots 0..iters-1 mod 4) as one graph.
-int build_graph(cgx_cg *cg, int iters) {
-  drop_graph(cg);
+// Capture `iters` iterations starting at slot `slot0` (slots slot0 ..
+// slot0 + iters - 1 mod 4) as one graph, cached under (slot0, iters).
+int build_graph(cgx_cg *cg, int slot0, int64_t iters, hipGraphExec_t *out) {
+  if (cg->graph_x != cg->x) drop_graph(cg);
   hipStream_t s = cg->ctx->stream;
   CGX_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   int rc = CGX_OK;
-  for (int i = 0; i < iters && rc == CGX_OK; ++i) rc = enqueue_iter_any(cg, i & 3);
+  for (int64_t i = 0; i < iters && rc == CGX_OK; ++i)
+    rc = enqueue_iter_any(cg, (int)((slot0 + i) & 3));
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(s, &g);
   if (rc) {
@@ -468,19 +459,37 @@ int build_graph(cgx_cg *cg, int iters) {
     return rc;
   }
   CGX_HIP(e);
-  e = hipGraphInstantiate(&cg->graph, g, nullptr, nullptr, 0);
+  hipGraphExec_t ge = nullptr;
+  e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   CGX_HIP(e);
   cg->graph_x = cg->x;
-  cg->graph_iters = iters;
+  cg->graphs[{slot0, iters}] = ge;
+  *out = ge;
   return CGX_OK;
 }
 
 bool graph_ok(const cgx_cg *cg) {
   // RCCL / host-transport calls are kept out of captured graphs (the peer
   // transport's iteration is all kernels); timing needs eager launches
-  return cg->use_graph && !cg->timing && (!cg->A->dist || cg->A->peer.on) &&
-         cg->poll_every % 4 == 0;
+  return cg->use_graph && !cg->timing && (!cg->A->dist || cg->A->peer.on);
+}
+
+// The graph for a chunk of `iters` bodies from `slot0`: a cached one, else a
+// new capture when `build` (full poll_every chunks, and cgx_cg_prepare),
+// else null (the chunk is launched eagerly).
+int chunk_graph(cgx_cg *cg, int slot0, int64_t iters, bool build, hipGraphExec_t *out) {
+  *out = nullptr;
+  if (cg->graph_x == cg->x) {
+    auto it = cg->graphs.find({slot0, iters});
+    if (it != cg->graphs.end()) {
+      *out = it->second;
+      return CGX_OK;
+    }
+  }
+  if (!build) return CGX_OK;
+  if (cg->graphs.size() >= 16) drop_graph(cg);  // bound the cache
+  return build_graph(cg, slot0, iters, out);
 }
 
 }  // namespace
@@ -588,6 +597,12 @@ extern "C" int cgx_get_stream(cgx_ctx *ctx, void **s) {
 extern "C" int cgx_get_device(cgx_ctx *ctx, int *d) {
   CGX_REQUIRE(ctx && d, CGX_EINVAL, "NULL argument");
   *d = ctx->device;
+  return CGX_OK;
+}
+
+extern "C" int cgx_max_work_group_size(cgx_ctx *ctx, int *size) {
+  CGX_REQUIRE(ctx && size, CGX_EINVAL, "NULL argument");
+  CGX_HIP(hipDeviceGetAttribute(size, hipDeviceAttributeMaxThreadsPerBlock, ctx->device));
   return CGX_OK;
 }
 
@@ -1468,7 +1483,18 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
               "variant %d needs SELL-P value codes, which this matrix does not have", variant);
   CGX_REQUIRE(!(variant & 262144) || A->dev.svc4, CGX_EUNSUPPORTED,
               "variant %d needs 4-bit value codes (at most 15 distinct values)", variant);
+  // the bit mask is not enough: check the form the request resolves to on
+  // this matrix has a kernel (e.g. 2138112, plane march without the pipe
+  // bits, has none)
+  const int old = A->dev.variant;
   A->dev.variant = variant;
+  if (!launch_variant_ok(A->dev, A->dtype)) {
+    const int resolved = launch_variant(A->dev, A->dtype);
+    A->dev.variant = old;
+    set_error("SpMV variant %d resolves to %d on this matrix, which has no kernel", variant,
+              resolved);
+    return CGX_EINVAL;
+  }
   return CGX_OK;
 }
 
@@ -1852,6 +1878,18 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
     CGX_HIP(hipMemsetAsync(cg->pk[2], 0, (size_t)cg->n * dtype_size(cg->dtype), s));
   const void *xe = x;
   int rc;
+  if (A->dist && A->peer.on) {
+    // PeerState::fault is sticky (every later peer kernel returns at entry):
+    // a matrix whose transport timed out once fails every later solve until
+    // cgx_dist_peer_enable rebuilds it, instead of skipping its all-reduces
+    int fault = 0;
+    CGX_HIP(hipMemcpyAsync(&fault, (const char *)A->peer.state + offsetof(PeerState, fault),
+                           sizeof(int), hipMemcpyDeviceToHost, s));
+    CGX_HIP(hipStreamSynchronize(s));
+    CGX_REQUIRE(!fault, CGX_ENCCL,
+                "peer transport: an earlier device-side wait on this matrix timed out; call "
+                "cgx_dist_peer_enable again (collectively) before the next solve");
+  }
   if (A->dist) {
     // initial guess with ghost values, staged in the Ap buffer (free at init)
     const size_t es = dtype_size(cg->dtype);
@@ -1906,8 +1944,7 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   DeviceGuard g(cg->ctx->device);
   hipStream_t s = cg->ctx->stream;
   const bool use_graph = graph_ok(cg);
-  if (use_graph && cg->graph && (cg->graph_x != cg->x || cg->graph_iters != cg->poll_every))
-    drop_graph(cg);
+  if (cg->graph_x != cg->x) drop_graph(cg);
   // Two host staging buffers: chunk c's state is read while chunk c+1 runs.
   auto *hbuf = (char *)cg->ctx->h_pinned;
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -1945,13 +1982,12 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   }
   while (!done && (remaining > 0 || !q.empty())) {
     if (remaining > 0 && q.size() < 2) {
-      int64_t chunk;
-      if (use_graph && cg->slot == 0 && remaining >= cg->poll_every) {
-        if (!cg->graph && (rc = build_graph(cg, cg->poll_every))) break;
-        CGX_HIP(hipGraphLaunch(cg->graph, s));
-        chunk = cg->poll_every;
+      const int64_t chunk = std::min<int64_t>(remaining, cg->poll_every);
+      hipGraphExec_t ge = nullptr;
+      if (use_graph && (rc = chunk_graph(cg, cg->slot, chunk, chunk == cg->poll_every, &ge))) break;
+      if (ge) {
+        CGX_HIP(hipGraphLaunch(ge, s));
       } else {
-        chunk = std::min<int64_t>(remaining, cg->poll_every);
         for (int64_t i = 0; i < chunk && rc == CGX_OK; ++i) rc = enqueue_iter_any(cg, (cg->slot + (int)i) & 3);
         if (rc) break;
       }
@@ -1984,6 +2020,38 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   }
   if (bodies_total) *bodies_total = last_bodies;
   if (stopped) *stopped = last_stopped;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_prepare(cgx_cg *cg, int64_t bodies) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  CGX_REQUIRE(cg->begun, CGX_ESTATE, "cgx_cg_prepare before cgx_cg_begin");
+  if (!graph_ok(cg) || bodies < 1) return CGX_OK;
+  DeviceGuard g(cg->ctx->device);
+  if (cg->graph_x != cg->x) drop_graph(cg);
+  // the chunk sequence cgx_cg_run(bodies) walks from the current slot
+  int slot = cg->slot;
+  for (int64_t remaining = bodies; remaining > 0;) {
+    const int64_t chunk = std::min<int64_t>(remaining, cg->poll_every);
+    hipGraphExec_t ge = nullptr;
+    if (int rc = chunk_graph(cg, slot, chunk, true, &ge)) return rc;
+    slot = (int)((slot + chunk) & 3);
+    remaining -= chunk;
+  }
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_rxr(cgx_cg *cg, double *rxr) {
+  CGX_REQUIRE(cg && rxr, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(cg->begun, CGX_ESTATE, "cgx_cg_rxr before cgx_cg_begin");
+  DeviceGuard g(cg->ctx->device);
+  auto *h = (char *)cg->ctx->h_pinned;
+  int rc;
+  if ((rc = poll_state(cg, h, cg->ctx->stream))) return rc;
+  CGX_HIP(hipStreamSynchronize(cg->ctx->stream));
+  // the rxr after the last body sits in the slot of the first skipped body
+  const long long bodies = view_state(cg, h, 0).bodies;
+  *rxr = view_state(cg, h, (int)(bodies & 3)).rxr;
   return CGX_OK;
 }
 

@@ -264,12 +264,22 @@ int dist_allreduce_scalar(cgx_ctx *ctx, void *d_val, int dtype, int count, hipSt
     auto *h = (char *)ctx->h_pinned + 512;  // [0, 512) is cgx_cg_run's poll staging
     CGX_HIP(hipMemcpyAsync(h, d_val, es * count, hipMemcpyDeviceToHost, s));
     CGX_HIP(hipStreamSynchronize(s));
-    int rc;
-    if ((rc = dist_async_status(ctx))) return rc;  // a failed exchange: stop before the collective
-    double v[8];
+    // a failed asynchronous exchange on this rank still enters the
+    // collective (its peers would otherwise wait in it forever) and carries
+    // the failure in a status word beside the values: all ranks fail together
+    const int mine = dist_async_status(ctx);
+    const std::string why = mine ? cgx_last_error() : "";
+    double v[9];
     for (int i = 0; i < count; ++i)
       v[i] = dtype == CGX_F32 ? (double)((float *)h)[i] : ((double *)h)[i];
-    CGX_CB(ctx->host->allreduce(ctx->host->user, v, count));
+    v[count] = mine ? 1.0 : 0.0;
+    CGX_CB(ctx->host->allreduce(ctx->host->user, v, count + 1));
+    if (mine) {
+      set_error("%s", why.c_str());
+      return mine;
+    }
+    CGX_REQUIRE(v[count] == 0.0, CGX_ENCCL,
+                "host transport: the halo exchange failed on %g other rank(s)", v[count]);
     for (int i = 0; i < count; ++i) {
       if (dtype == CGX_F32) ((float *)h)[i] = (float)v[i];
       else ((double *)h)[i] = v[i];

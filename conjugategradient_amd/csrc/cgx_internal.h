@@ -185,11 +185,6 @@ template <typename T> struct Launch {
                                          int part_off, const T *p, T *Ap, CgScalars<T> *st,
                                          int slot, RedWs<T> *ws, hipStream_t s, int rev,
                                          const PeerDev &P, int wg0);
-  // the boundary slices with the halo wait in the launch's first kWaitWG
-  // workgroups (k_spmv_dot_wait); its SpMV workgroups: slice_grid_push(.., kWaitWG)
-  static hipError_t spmv_dot_slices_wait(const CsrDev &A, const int *list, int count,
-                                         int part_off, T *p, T *Ap, CgScalars<T> *st, int slot,
-                                         RedWs<T> *ws, hipStream_t s, int rev, const PeerDev &P);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);
@@ -240,6 +235,10 @@ enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 
 // the SpMV variant a launch on A uses (dtype: CGX_F64 / CGX_F32)
 int launch_variant(const CsrDev &A, int dtype);
+// true when the variant A resolves to (launch_variant) has a k_spmv_dot
+// instantiation: a request that resolves to anything else would only fail
+// at its first launch
+bool launch_variant_ok(const CsrDev &A, int dtype);
 
 // host-side row-block schedule (cgx_abi.cpp)
 std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz,

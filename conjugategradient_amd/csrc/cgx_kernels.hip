@@ -2151,30 +2151,6 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
 }
 
-// The boundary SpMV of a partitioned SELL matrix with the peer transport's
-// halo wait in its first A.wg0 (= kWaitWG) workgroups (peerdev::wait_wg, as
-// k_peer_wait): the SpMV workgroups first wait for their ready flags
-// (peerdev::ghosts_ready), then run the boundary slices; one launch instead
-// of two. Partials at part_off + blockIdx - wg0.
-template <typename T, int V>
-__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_wait(
-    CsrArgs A, const T *__restrict__ val, T *__restrict__ p, T *__restrict__ Ap,
-    CgScalars<T> *st, int slot, RedWs<T> *ws, PeerDev P) {
-  __shared__ int ok_s;
-  if ((int)blockIdx.x < A.wg0) {
-    peerdev::wait_wg<T>(p, P, st, slot, blockIdx.x, A.wg0, &ok_s);
-    return;
-  }
-  if (!st->active[slot] || P.state->fault) return;
-  if (!peerdev::ghosts_ready<T>(P, st, slot, A.wg0, &ok_s)) return;
-  __shared__ LdsOf<T, V> sm;
-  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
-  spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
-}
-
 // Fused deferred-x iteration (mode 4), kernel 1 of 2 for body k in slot s
 // (cgx_abi.cpp enqueue_iter_fdefer): p_k into P[s] from r and P[s-1] (EpiFD),
 // helper = A p_k, this workgroup's p.Ap partial. beta_{k-1} = r.r / rxr from
@@ -2390,8 +2366,11 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   if constexpr (PEER) {
     __shared__ double wres;
     __shared__ int wok;
-    if (P->state->fault) return;
-    if (!peerdev::world_sum((double)pAp, P->state->arb[slot & 1] + 1, *P, blockIdx.x == 0,
+    if (P->state->fault) {  // an earlier spin timed out: stop this body too
+      peer_fault(st, slot, P);
+      return;
+    }
+    if (!peerdev::world_sum((double)pAp, P->state->arb[slot & 1] + 1, *P,
                             &wres, &wok)) {
       peer_fault(st, slot, P);
       return;
@@ -2503,8 +2482,11 @@ __device__ __forceinline__ void update_xp_body(int64_t n, T *__restrict__ x, T *
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
-    if (P->state->fault) return;
-    if (!peerdev::world_sum((double)rr, P->state->arb[slot & 1] + 2, *P, blockIdx.x == 0, &wres,
+    if (P->state->fault) {  // an earlier spin timed out: stop this body too
+      peer_fault(st, slot, P);
+      return;
+    }
+    if (!peerdev::world_sum((double)rr, P->state->arb[slot & 1] + 2, *P, &wres,
                             &wok)) {
       peer_fault(st, slot, P);
       return;
@@ -2906,8 +2888,11 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
-    if (PD->state->fault) return;
-    if (!peerdev::world_sum((double)rr, PD->state->arb[slot & 1] + 2, *PD, blockIdx.x == 0,
+    if (PD->state->fault) {  // an earlier spin timed out: stop this body too
+      peer_fault(st, slot, PD);
+      return;
+    }
+    if (!peerdev::world_sum((double)rr, PD->state->arb[slot & 1] + 2, *PD,
                             &wres, &wok)) {
       peer_fault(st, slot, PD);
       return;
@@ -3482,36 +3467,6 @@ template <typename T> static const void *spmv_push_kernel(int v) {
   }
 }
 
-template <typename T> static const void *spmv_wait_kernel(int v) {
-  switch (v) {
-#define CGX_KWA(VV) \
-  case VV: return reinterpret_cast<const void *>(&k_spmv_dot_wait<T, VV>);
-    CGX_PUSH_LIST(CGX_KWA)
-#undef CGX_KWA
-    default: return nullptr;
-  }
-}
-template <typename T>
-hipError_t Launch<T>::spmv_dot_slices_wait(const CsrDev &A, const int *list, int count,
-                                           int part_off, T *p, T *Ap, CgScalars<T> *st, int slot,
-                                           RedWs<T> *ws, hipStream_t s, int rev, const PeerDev &P) {
-  const int v = spmv_variant<T>(A) & ~2097152;
-  const void *k = spmv_wait_kernel<T>(v);
-  if (!k || count < 1) return hipErrorInvalidValue;
-  CsrArgs a = args(A);
-  a.sorder = list;
-  a.nsl = count;
-  a.part_off = part_off;
-  a.rev = rev;
-  a.wg0 = kWaitWG;
-  const T *val = (const T *)A.val;
-  PeerDev pd = P;
-  void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
-                   (void *)&ws, (void *)&pd};
-  return hipLaunchKernel(k, dim3(kWaitWG + slice_grid_push(A, count, kWaitWG)), dim3(kBlock),
-                         kargs, 0, s);
-}
-
 template <typename T> bool Launch<T>::push_supported(const CsrDev &A) {
   return spmv_push_kernel<T>(spmv_variant<T>(A) & ~2097152) != nullptr;
 }
@@ -3667,6 +3622,11 @@ hipError_t Launch<T>::sell_pack(const CsrDev &A, const T *val, T *sval, hipStrea
 
 int launch_variant(const CsrDev &A, int dtype) {
   return dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A);
+}
+
+bool launch_variant_ok(const CsrDev &A, int dtype) {
+  return dtype == 1 /* CGX_F32 */ ? spmv_dot_kernel<float>(spmv_variant<float>(A)) != nullptr
+                                  : spmv_dot_kernel<double>(spmv_variant<double>(A)) != nullptr;
 }
 
 template <typename T>

@@ -7,7 +7,9 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdint>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/cgx.h"
@@ -58,7 +60,6 @@ struct Halo {
 // a partitioned iteration is all kernels and graph-capturable.
 constexpr int kPeerMax = 16;  // ranks of one node
 constexpr int kPushWG = 16;   // push workgroups (and flags) per neighbour
-constexpr int kWaitWG = 8;    // halo wait workgroups leading the boundary SpMV launch
 struct PeerState {            // device, per matrix
   unsigned long long ar;      // all-reduces completed (the tag of the last)
   int fault;                  // a spin timed out: every later peer kernel returns
@@ -68,9 +69,11 @@ struct PeerState {            // device, per matrix
   // arb[(s + 1) & 1] (read by no kernel of this body, so the all-reduce can
   // run inside a many-workgroup consumer kernel)
   unsigned long long arb[2];
-  // k_spmv_dot_wait: wait workgroup w raises ready[w] to the body's tag once
-  // its share of the ghosts is in place; the boundary slices wait for all
-  unsigned long long ready[kWaitWG];
+  // the highest all-reduce tag a workgroup of a consumer kernel has claimed
+  // to publish (peerdev::world_sum): the first workgroup to arrive for a tag
+  // publishes it, whichever it is, so no workgroup waits on one that may not
+  // be resident
+  unsigned long long pub;
 };
 struct PeerDev {  // kernel argument (by value)
   char *ctl[kPeerMax];            // rank q's mailbox + flags, as mapped here
@@ -185,11 +188,11 @@ struct cgx_cg {
   bool begun = false;
   int poll_every = 32;
   bool use_graph = true;
-  // graph of `poll_every` iterations starting at slot 0
-  hipGraphExec_t graph = nullptr;
-  const void *graph_b = nullptr;
+  // captured iterations, keyed by (first slot, bodies): full chunks of
+  // `poll_every` from any slot (built on first use) and the chunks
+  // cgx_cg_prepare built ahead of a run; all captured for x = graph_x
+  std::map<std::pair<int, int64_t>, hipGraphExec_t> graphs;
   void *graph_x = nullptr;
-  int graph_iters = 0;
   // kernel timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;

@@ -312,8 +312,20 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
   cgx_ctx *ctx = A->ctx;
   CGX_HIP(hipSetDevice(ctx->device));
   if (A->peer.on) {
-    *enabled = 1;
-    return CGX_OK;
+    // already on: keep it unless a spin timed out on any rank (the fault is
+    // sticky, cgx_cg_begin refuses such a matrix); then every rank rebuilds
+    // it together
+    int fault = 0;
+    CGX_HIP(hipMemcpy(&fault, (const char *)A->peer.state + offsetof(PeerState, fault),
+                      sizeof(int), hipMemcpyDeviceToHost));
+    int all_clean = 0;
+    if (int rc0 = all_ok(ctx, fault ? 0 : 1, &all_clean)) return rc0;
+    if (all_clean) {
+      *enabled = 1;
+      return CGX_OK;
+    }
+    CGX_HIP(hipStreamSynchronize(ctx->stream));
+    peer_destroy(A);
   }
   const int world = ctx->world, me = ctx->rank;
   int mine_ok = 1;

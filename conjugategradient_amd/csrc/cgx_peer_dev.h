@@ -48,15 +48,26 @@ __device__ __forceinline__ bool spin_ge(const unsigned long long *p, unsigned lo
 }
 
 // The world sum of `mine` (this rank's local sum, the same in every
-// workgroup of the calling kernel) for all-reduce tag t: the publisher
-// workgroup stores value and tag into every rank's mailbox, every workgroup
-// polls its own mailbox until all ranks' tags arrived and sums the values in
-// rank order (bit-identical everywhere). Uniform control flow; thread 0's
-// lds slots carry the result. false: a spin timed out.
+// workgroup of the calling kernel) for all-reduce tag t: the first workgroup
+// of the kernel to arrive here stores value and tag into every rank's
+// mailbox, every workgroup polls its own mailbox until all ranks' tags
+// arrived and sums the values in rank order (bit-identical everywhere).
+// The publisher is chosen by an agent-scope claim on PeerState::pub (a
+// plain load first, so only the early arrivals contend), never by a
+// workgroup index: the workgroup that publishes is one that is running, so
+// the spins never wait on a workgroup that is not yet resident (dispatch
+// order is undefined). Uniform control flow; thread 0's lds slots carry the
+// result. false: a spin timed out.
 __device__ __forceinline__ bool world_sum(double mine, unsigned long long t, const PeerDev &P,
-                                          bool publisher, double *res_lds, int *ok_lds) {
+                                          double *res_lds, int *ok_lds) {
   const int par = (int)(t & 1);
   if (threadIdx.x < 64) {
+    int claim = 0;
+    if (threadIdx.x == 0)
+      claim = __hip_atomic_load(&P.state->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t &&
+              __hip_atomic_fetch_max(&P.state->pub, t, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) < t;
+    const bool publisher = __shfl(claim, 0, 64) != 0;
     bool ok = true;
     if ((int)threadIdx.x < P.world) {
       if (publisher) {
@@ -121,74 +132,6 @@ __device__ __forceinline__ void raise_fault(CgScalars<T> *st, int slot, PeerStat
     st->active[slot] = 0;
     st->stopped = 3;
   }
-}
-
-// Halo wait workgroup w of nw leading the boundary SpMV launch (as
-// k_peer_wait): its first wave polls every sending rank's flags for this
-// body's tag, the workgroup copies its share of the landing buffer into v's
-// ghost area, then raises ready[w] (agent-scope release after its stores).
-template <typename T>
-__device__ __forceinline__ void wait_wg(T *__restrict__ v, const PeerDev &P, CgScalars<T> *st,
-                                        int slot, int w, int nw, int *ok_lds) {
-  if (skip_body(st, slot, P.state)) return;
-  const unsigned long long tag = body_tag(st, slot, P.state);
-  if (threadIdx.x < 64) {
-    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
-    bool ok = true;
-    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
-      ok = ok && spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
-                         P.spin_ticks);
-    ok = __all(ok);
-    if (threadIdx.x == 0) *ok_lds = ok;
-  }
-  __syncthreads();
-  if (!*ok_lds) {
-    if (threadIdx.x == 0) raise_fault(st, slot, P.state);
-    return;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
-  const T *land = reinterpret_cast<const T *>(P.land_local);
-  for (int64_t k = (int64_t)w * kBlock + threadIdx.x; k < P.n_ghost; k += (int64_t)nw * kBlock)
-    v[P.n_local + k] = land[k];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(&P.state->ready[w], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// A boundary-SpMV workgroup of that launch: wait until every wait workgroup
-// raised its ready flag for this body (bounded; a fault anywhere returns
-// false), then acquire at agent scope so the ghosts are seen.
-template <typename T>
-__device__ __forceinline__ bool ghosts_ready(const PeerDev &P, CgScalars<T> *st, int slot, int nw,
-                                             int *ok_lds) {
-  const unsigned long long tag = body_tag(st, slot, P.state);
-  if (threadIdx.x < 64) {
-    bool ok = true;
-    if ((int)threadIdx.x < nw) {
-      const long long t0 = wall_clock64();
-      while (__hip_atomic_load(&P.state->ready[threadIdx.x], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT) < tag) {
-        if (__hip_atomic_load(&P.state->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-            wall_clock64() - t0 > P.spin_ticks) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    ok = __all(ok);
-    if (threadIdx.x == 0) *ok_lds = ok;
-  }
-  __syncthreads();
-  if (!*ok_lds) {
-    if (threadIdx.x == 0) raise_fault(st, slot, P.state);
-    return false;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return true;
 }
 
 }  // namespace peerdev

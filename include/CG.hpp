@@ -15,6 +15,7 @@
  * few iterations.
  */
 #include <AdaptiveCpp/sycl/sycl.hpp>
+#include <algorithm>
 #include <cassert>
 #include <cmath>
 #include <cstdint>
@@ -108,6 +109,9 @@ template <typename DT, Debuglevel debug = Debuglevel::None> class CG {
    */
   void solve(DT improvement = static_cast<DT>(0)) {
     if constexpr (debug == Debuglevel::Verbose) std::clog << "Solving System\n";
+    // :260-261 (its constructor prints the work-group line under Verbose)
+    VectorOperations<DT, debug> vecops(this->_queue);
+    vecops.setVectorSize(A.N());
     if (this->b.data() == nullptr) throw std::runtime_error("No right hand side to solve for");
     if (this->A.columns().get() == nullptr) throw std::runtime_error("No Matrix given");
     const auto N = A.N();
@@ -115,17 +119,37 @@ template <typename DT, Debuglevel debug = Debuglevel::None> class CG {
       if constexpr (debug == Debuglevel::Verbose) std::clog << "x init empty" << std::endl;
       x.init_empty(N);
     }
-    cgx_cg *s = solver();
-    if constexpr (debug == Debuglevel::Verbose) std::clog << "Entering Loop" << std::endl;
+    cgx_cg *s = solver();  // the solver's vectors and scalars (:276-302)
+    if constexpr (debug == Debuglevel::Verbose) std::clog << "Prepared Memory" << std::endl;
+    // :314-341: r = b - A x, p = r, rxr = r.r
+    check(cgx_cg_begin(s, b.ptr(), x.ptr(), (double)improvement, _max_iterations), "solve");
+    if constexpr (debug == Debuglevel::Verbose) {
+      check(cgx_sync(_queue.native()), "solve");
+      std::clog << "Init done" << std::endl;
+      std::clog << "Entering Loop" << std::endl;
+    }
+    // :359-436: at most N + 1 bodies (or the extension's cap)
+    int64_t cap = static_cast<int64_t>(N) + 1;
+    if (_max_iterations >= 0) cap = std::min<int64_t>(cap, std::max<int64_t>(_max_iterations, 1));
     int64_t bodies = 0;
+    int stopped = 0;
+    check(cgx_cg_run(s, cap, &bodies, &stopped), "solve");
     double rxr = 0;
-    check(cgx_cg_solve(s, b.ptr(), x.ptr(), (double)improvement, _max_iterations, &bodies, &rxr),
-          "solve");
+    check(cgx_cg_rxr(s, &rxr), "solve");  // :437-440
     _iterations = bodies;
     _final_rxr = rxr;
     this->is_solved = true;
     if constexpr (debug == Debuglevel::Verbose) {
-      std::clog << bodies << " iterations" << std::endl;
+      // :428-434: the progress line the reference writes after every body
+      // whose counter is a multiple of 100, in the same order and format
+      // (written here once the device loop has finished: the loop does not
+      // return to the host per body)
+      for (int64_t counter = 0; counter < bodies; counter += 100) {
+        std::clog << "\r\033[2K";
+        std::clog << ((static_cast<double>(counter) / N) * 100) << "%";
+        std::flush(std::clog);
+      }
+      std::clog << std::endl;  // :450-453
       std::clog << "Finished solving" << std::endl;
     }
   }

@@ -119,12 +119,17 @@ template <class DT, Debuglevel debug = Debuglevel::None> class VectorOperations 
     return asycl::event(_queue);
   }
 
-  // :478-487 — the reference picks min(128, max work-group size); the gfx950
-  // kernels run 256-thread workgroups, the value is kept for interface parity
+  // :478-487 — the reference picks min(128, the device's max work-group
+  // size); the gfx950 kernels run 256-thread workgroups, the value is kept
+  // for interface parity
   size_t calculateWorkgroupSize() {
+    int max_wg = 0;
+    asycl::detail::check(cgx_max_work_group_size(_queue.native(), &max_wg),
+                         "max_work_group_size");
+    const size_t max_wg_size = static_cast<size_t>(max_wg);
     if constexpr (debug == Debuglevel::Verbose)
-      std::clog << "work group size is " << 1024 << std::endl;
-    return std::min(static_cast<size_t>(128), static_cast<size_t>(1024));
+      std::clog << "work group size is " << max_wg_size << std::endl;
+    return std::min(static_cast<size_t>(128), max_wg_size);
   }
 
   size_t workgroupsize;

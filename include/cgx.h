@@ -50,6 +50,9 @@ int cgx_destroy(cgx_ctx *ctx);
 int cgx_sync(cgx_ctx *ctx);                          /* executeQueue :561-578 */
 int cgx_get_stream(cgx_ctx *ctx, void **hip_stream);
 int cgx_get_device(cgx_ctx *ctx, int *device);
+/* the device's max_work_group_size (VectorOperations.hpp:478-487 queries it
+ * through sycl::info::device::max_work_group_size) */
+int cgx_max_work_group_size(cgx_ctx *ctx, int *size);
 
 /* ---- memory: replaces sycl::malloc_device/free/copy/fill ------------------
  * (LinearAlgebraTypes.hpp:43-49 Asycl_deleter, :109-119 Matrix::init,
@@ -151,6 +154,14 @@ int cgx_cg_solve(cgx_cg *cg, const void *d_b, void *d_x, double tol,
 int cgx_cg_begin(cgx_cg *cg, const void *d_b, void *d_x, double tol,
                  int64_t max_bodies);
 int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int *stopped);
+/* Capture, ahead of time, the hipGraphs a following cgx_cg_run(cg, bodies)
+ * replays (chunks of the poll interval from the current slot; a run builds
+ * only full chunks itself and launches a shorter tail eagerly). Blocking
+ * host work, no kernel runs. Benchmarks call it before a timed run. */
+int cgx_cg_prepare(cgx_cg *cg, int64_t bodies);
+/* r.r after the last body run so far (the value the reference reads back
+ * after its loop, CG.hpp:437-440); blocking. */
+int cgx_cg_rxr(cgx_cg *cg, double *rxr);
 /* Per-kernel device time, accumulated with HIP events on the solver stream
  * while enabled: avg_ms[0..3] = init, spmv_dot, update_r, update_xp;
  * calls[0..3] = launches timed. */

@@ -90,8 +90,46 @@ def test_reference_tester_runs_on_gpu(name, exe):
     g = np.load(os.path.join(GOLD, f"loader_{name}.npz"))
     assert n == len(g["rowptr"]) - 1 and nnz == len(g["val"])
     # Tester.cpp solves to 1e-24; accuracy() = ||b-Ax||^2/||x||^2 (Q6)
-    gold = float(np.load(os.path.join(GOLD, f"cg_{name}.npz"))["accuracy_1e-24"])
-    assert acc < 1e-24 and acc < 100 * gold
+    gold = np.load(os.path.join(GOLD, f"cg_{name}.npz"))
+    assert acc < 1e-24 and acc < 100 * float(gold["accuracy_1e-24"])
+    _check_verbose_trace(p.stderr, n, int(gold["iters_1e-24"]))
+
+
+# The std::clog sequence a Debuglevel::Verbose solver prints for Tester.cpp's
+# calls (createCG, setMatrix, setTarget, solve, extract, getDimension,
+# accuracy), in the reference's order and text:
+REF_TRACE_HEAD = [
+    r"Constructing CG Object",        # CG.hpp:63-64
+    r"Setting Matrix",                # CG.hpp:89-90
+    r"Solving System",                # CG.hpp:257-258
+    r"work group size is \d+",        # VectorOperations.hpp:484-485 (vecops, CG.hpp:260)
+    r"x init empty",                  # CG.hpp:292-295
+    r"Prepared Memory",               # CG.hpp:306-308
+    r"Init done",                     # CG.hpp:337-339
+    r"Entering Loop",                 # CG.hpp:356-358
+]
+REF_TRACE_TAIL = [r"Finished solving", r"Calculating accuracy"]  # CG.hpp:450-453, :465-466
+
+
+def _check_verbose_trace(stderr, n, oracle_bodies):
+    lines = [ln for ln in stderr.split("\n") if "amdgpu.ids" not in ln]
+    while lines and lines[-1] == "":
+        lines.pop()
+    head, prog, tail = lines[:len(REF_TRACE_HEAD)], lines[len(REF_TRACE_HEAD)], \
+        lines[len(REF_TRACE_HEAD) + 1:]
+    assert len(head) == len(REF_TRACE_HEAD) and all(
+        re.fullmatch(w, h) for w, h in zip(REF_TRACE_HEAD, head)), lines
+    assert tail == REF_TRACE_TAIL, lines
+    # CG.hpp:428-434: "\r\033[2K" then (counter / N) * 100 and "%" after every
+    # body whose counter is a multiple of 100 (default ostream format: %g);
+    # the loop's std::endl (:451) ends the line
+    steps = prog.split("\r\033[2K")
+    assert steps[0] == "" and len(steps) >= 2, repr(prog)
+    want = [f"{(100.0 * k / n) * 100:g}%" for k in range(len(steps) - 1)]
+    assert steps[1:] == want, (steps[1:], want)
+    # one line per started hundred bodies; the body count at 1e-24 follows
+    # the summation order (report only), so a band
+    assert abs(100 * (len(steps) - 1) - oracle_bodies) <= 100 + 0.1 * oracle_bodies
 
 
 @pytest.mark.gpu

@@ -64,16 +64,6 @@ def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
     assert r["peer"] == [int(transport.endswith("-peer"))] * nproc
 
 
-def test_folded_halo_wait(monkeypatch):
-    """$CGX_PEER_WAIT_FOLD=1: the halo wait rides in the boundary SpMV
-    launch's first workgroups (k_spmv_dot_wait), the boundary slices wait on
-    their ready flags; same x as the oracle at 3 ranks."""
-    monkeypatch.setenv("CGX_PEER_WAIT_FOLD", "1")
-    r = _run(3, "host-peer", 20, 3)
-    assert r["ok"], r
-    assert r["peer"] == [1, 1, 1]
-
-
 @pytest.mark.parametrize("nproc,grid,mode", [(2, 24, 0), (3, 20, 3)])
 def test_async_host_halo_matches_synchronous(nproc, grid, mode):
     """The overlapped halo ordering of the RCCL branch (cgx_dist.cpp
@@ -103,3 +93,22 @@ def test_partitioned_slab_of_the_8gpu_config():
     assert r["bodies"] == 40 and r["grid"] == [512, 512, 128]
     assert r["ghosts"] == [512 * 512, 512 * 512]  # one plane from the other slab
     assert all(ni > 0 and nb > 0 for ni, nb in r["split"]), r["split"]
+
+
+def test_bench_two_ranks_validates_peer_transport():
+    """bench.py at N > 1 uses the device peer transport only after
+    validate_peer solved a small slab problem over it and over the setup
+    transport to the same answer (accuracy, bodies +-2, x to 1e-10). On the
+    one-GPU box the setup transport is the host one (--transport host-peer);
+    on an 8-GPU node it is RCCL (--transport auto)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--grid", "64",
+           "--steps", "20", "--warmup", "5", "--transport", "host-peer", "--no-cpu",
+           "--profile-steps", "0", "--master-port", str(_port())]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 20
+    v = line["config"]["transport_validation"]
+    assert v["ok"], v
+    assert v["x_rel_peer_vs_setup"] <= 1e-10
+    assert line["config"]["transport"].startswith("peer")
