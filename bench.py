@@ -93,9 +93,13 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--grid", type=int, default=256,
-                    help="n of the global n^3 grid (strong scaling, the default), or of each "
-                         "rank's slab with --weak")
+    ap.add_argument("--workload", default="p3d_256",
+                    choices=["p3d_256", "p3d_512", "p2d_4096", "p2d_128", "g3_standin"],
+                    help="BASELINE.json configuration (conjugategradient_amd/workloads.py); "
+                         "the default is the headline 256^3 one; N > 1 takes the 3-D ones")
+    ap.add_argument("--grid", type=int, default=None,
+                    help="n of the global n^3 grid of a 3-D workload (strong scaling, the "
+                         "default), or of each rank's slab with --weak; --grid 512 is p3d_512")
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: every rank owns an n^3 slab of an n x n x (n N) grid")
     ap.add_argument("--strong", action="store_true", help=argparse.SUPPRESS)  # the default
@@ -122,6 +126,9 @@ def parse(argv=None):
                          "host (host-staged test transport: lets ranks share one GPU; "
                          "rehearsal only, numbers meaningless), host-peer (host setup, "
                          "device peer iteration: a one-GPU rehearsal of the peer path)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 PMC passes that measure roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--master-port", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -196,16 +203,26 @@ def job_cores() -> dict:
             "nproc": os.cpu_count(), "model": model}
 
 
-def cpu_baseline(n3: int, threads: int, budget_s: float):
+def cpu_baseline(workload: str, grid, threads: int, budget_s: float):
     """The oracle's OpenMP restatement of the reference iteration on a sample
     of the same workload (same matrix, same b), timed on host cores."""
     import numpy as np
     from oracle import oracle as O
 
+    from conjugategradient_amd import workloads
+
     info = job_cores()
     if threads <= 0:
         threads = info["use"]
-    rp, cl, vl = O.poisson(3, n3, n3, n3)
+    if workload in workloads.POISSON:
+        dim, nx, ny, nz = workloads.POISSON[workload]
+        if grid and dim == 3:
+            nx = ny = nz = grid
+        rp, cl, vl = O.poisson(dim, nx, ny, nz)
+        what = f"{nx}^3 7-pt Poisson" if dim == 3 else f"{nx}^2 5-pt Poisson"
+    else:
+        rp, cl, vl = workloads.host_csr(workload)
+        what = workload
     n, nnz = len(rp) - 1, len(vl)
     b = np.arange(1, n + 1, dtype=np.float64)
     t1, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, 2, threads)  # probe (also warms the pool)
@@ -222,7 +239,7 @@ def cpu_baseline(n3: int, threads: int, budget_s: float):
                  "affinity_cores": info["affinity"], "cgroup_cpu_quota": info["cgroup_quota"],
                  "declared_cpu_share": info["declared_share"],
                  "omp_proc_bind": os.environ.get("OMP_PROC_BIND")},
-        "sample": f"{n3}^3 7-pt Poisson, {iters} iterations of the reference command "
+        "sample": f"{what}, {iters} iterations of the reference command "
                   f"sequence (oracle/cg_oracle.c orc_cg_fixed_iters_omp, OpenMP, "
                   f"{threads} threads), {its:.3f} it/s, {t:.2f} s; value priced at the "
                   f"CSR bytes B_alg",
@@ -238,6 +255,7 @@ def run(args) -> None:
     import torch.distributed as dist
 
     import conjugategradient_amd as cga
+    from conjugategradient_amd import workloads
     from conjugategradient_amd._native import F64, check, lib
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,20 +266,7 @@ def run(args) -> None:
     dev = local % max(1, cga.device_count())
     L = lib()
     q = cga.Queue(dev)
-    n3 = args.grid
     strong = not args.weak
-    if strong:
-        if n3 % world:
-            raise SystemExit(f"strong scaling needs the grid ({n3}) divisible by the GPU "
-                             f"count ({world})")
-        nz_global = n3
-        n_local = n3 * n3 * (n3 // world)
-    else:
-        nz_global = n3 * world
-        n_local = n3 * n3 * n3
-    row_begin = rank * n_local
-    n_global = n_local * world
-
     # ---- communicator (N > 1) ----------------------------------------------
     transport = "single"
     if world > 1 and args.transport in ("host", "host-peer"):
@@ -283,25 +288,22 @@ def run(args) -> None:
         raise SystemExit(f"bench.py: communicator world {ww.value}, --gpus {args.gpus}, "
                          f"WORLD_SIZE {world}: they must match")
 
-    # ---- inputs generated in HBM ---------------------------------------------
-    nnz_local = L.cgx_poisson_nnz(3, n3, n3, nz_global, row_begin, row_begin + n_local)
-    nnz_global = L.cgx_poisson_nnz(3, n3, n3, nz_global, 0, n_global)
-    rows = cga.DeviceArray(q, n_local + 1, np.int32)
-    cols = cga.DeviceArray(q, nnz_local, np.int32)
-    vals = cga.DeviceArray(q, nnz_local, np.float64)
-    check(L.cgx_poisson_fill(q.handle, F64, 3, n3, n3, nz_global, row_begin,
-                             row_begin + n_local, rows.ptr, cols.ptr, vals.ptr))
+    # ---- inputs in HBM (conjugategradient_amd/workloads.py) -------------------
+    wl = workloads.build(L, q, args.workload, world, rank, args.grid, args.weak)
+    n_local, nnz_local, n_global, nnz_global = wl.n_local, wl.nnz_local, wl.n_global, \
+        wl.nnz_global
+    row_begin = wl.row_begin
     b = cga.DeviceArray(q, n_local, np.float64)
     x = cga.DeviceArray(q, n_local, np.float64)
     check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(row_begin)))
     x.fill(0.0)
     A = C.c_void_p()
     if world > 1:
-        check(L.cgx_csr_create_dist(q.handle, n_global, row_begin, n_local, nnz_local, rows.ptr,
-                                    cols.ptr, vals.ptr, F64, C.byref(A)))
+        check(L.cgx_csr_create_dist(q.handle, n_global, row_begin, n_local, nnz_local,
+                                    wl.rows.ptr, wl.cols.ptr, wl.vals.ptr, F64, C.byref(A)))
     else:
-        check(L.cgx_csr_create(q.handle, n_local, nnz_local, rows.ptr, cols.ptr, vals.ptr, F64,
-                               None, C.byref(A)))
+        check(L.cgx_csr_create(q.handle, n_local, nnz_local, wl.rows.ptr, wl.cols.ptr,
+                               wl.vals.ptr, F64, None, C.byref(A)))
     peer_note = None
     validation = None
     use_peer = world > 1 and args.transport in ("peer", "host-peer")
@@ -360,6 +362,10 @@ def run(args) -> None:
     check(L.cgx_cg_run(cg, args.steps, C.byref(bodies), C.byref(stopped)))
     q.wait()
     t1 = time.perf_counter()
+    if args.pmc_child:  # a PMC pass of pmc_traffic: the dispatches are what it needs
+        check(L.cgx_cg_destroy(cg))
+        check(L.cgx_csr_destroy(A))
+        return
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -415,18 +421,18 @@ def run(args) -> None:
             roof["other_kernels_avg_us"]["k_flush_group"] = round(avg[3] * 1e3, 2)
         elif not fused:
             roof["other_kernels_avg_us"]["k_update_p"] = round(avg[3] * 1e3, 2)
-        pmc = os.path.join(ROOT, "profiles", "pmc_spmv_dot.json")
-        if os.path.exists(pmc):
-            try:
-                meta = json.load(open(pmc))
-                # PMC bytes of this very kernel: same per-GPU grid, variant, mode
-                if (meta.get("grid") == n3 and world == 1
-                        and meta.get("spmv_variant") == variant.value
-                        and meta.get("kernel") == roof["kernel"]):
-                    roof["traffic"] = meta.get("hbm_bytes_per_launch")
-                    roof["traffic_source"] = "profiles/pmc_spmv_dot.json"
-            except Exception:
-                pass
+        if world == 1 and not args.no_traffic:
+            # HBM bytes per launch from rocprofv3 PMC passes of this same
+            # workload, variant and mode (child processes, after this run)
+            t = pmc_traffic(args, int(variant.value), mode_eff)
+            roof["traffic_by_kernel"] = t.get("by_kernel")
+            roof["traffic_method"] = t.get("method")
+            key = f"{kname}<double, {int(variant.value)}>"
+            if t.get("by_kernel") and key in t["by_kernel"]:
+                roof["traffic"] = t["by_kernel"][key]
+                roof["traffic_ratio_to_compulsory"] = round(roof["traffic"] / kb, 4)
+            else:
+                roof["traffic_error"] = t.get("error") or f"no PMC samples for {key}"
 
     # ---- general-value formats on the same matrix (N = 1) --------------------------
     general = None
@@ -436,12 +442,11 @@ def run(args) -> None:
     line = None
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu and n3 <= 256:
+        big = args.workload == "p3d_512" or (args.grid or 0) > 256
+        if world == 1 and not args.no_cpu and not big:
             os.environ.setdefault("OMP_PROC_BIND", "close")
-            cpu = cpu_baseline(n3, args.cpu_threads, args.cpu_budget_s)
-        workload = (f"3D 7-pt Poisson {n3}^3 global, {nz_global // world} z-planes per GPU"
-                    if strong else
-                    f"3D 7-pt Poisson {n3}^3 per GPU (global {n3}x{n3}x{nz_global})")
+            cpu = cpu_baseline(args.workload, args.grid, args.cpu_threads, args.cpu_budget_s)
+        workload = wl.description
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -455,8 +460,9 @@ def run(args) -> None:
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (3-D 7-point Dirichlet Poisson CSR generated in HBM, "
-                    "b_i = i + 1, x0 = 0)",
+            "data": ("synthetic (Dirichlet Poisson CSR generated in HBM, b_i = i + 1, x0 = 0)"
+                     if args.workload in workloads.POISSON else
+                     "synthetic (see config.workload; b_i = i + 1, x0 = 0)"),
             "value_basis": "compulsory HBM bytes per iteration in the streamed formats "
                            "(all ranks) x iterations/s",
             "bytes_per_iteration": iter_global,
@@ -465,6 +471,7 @@ def run(args) -> None:
             "csr_equivalent_bytes_per_iteration": b_alg(n_global, nnz_global),
             "config": {"workload": workload + ", CSR fp64/int32 input, SpMV in the "
                                               "per-matrix best format",
+                       "workload_id": args.workload,
                        "rows_global": n_global, "nnz_global": nnz_global,
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
@@ -488,6 +495,86 @@ def run(args) -> None:
         dist.destroy_process_group()
 
 
+def kernel_base_name(full: str) -> str:
+    """'void cgx::(anonymous namespace)::k_x<double, 5>(args...)' -> 'k_x<double, 5>'."""
+    name = full.replace("(anonymous namespace)::", "")
+    return name.split("(")[0].replace("void ", "").replace("cgx::", "").strip()
+
+
+def pmc_accumulate(f, ctr: str, sums: dict) -> None:
+    """Add one rocprofv3 counter_collection.csv (open file) to sums[kernel][ctr]
+    = [total, dispatches]."""
+    import csv
+
+    for r in csv.DictReader(f):
+        if r.get("Counter_Name") != ctr:
+            continue
+        acc = sums.setdefault(kernel_base_name(r["Kernel_Name"]), {}).setdefault(ctr, [0.0, 0])
+        acc[0] += float(r["Counter_Value"])
+        acc[1] += 1
+
+
+def pmc_bytes(sums: dict) -> dict:
+    """HBM bytes per dispatch per kernel: (2 FETCH_SIZE + WRITE_SIZE) KB x 1024."""
+    out = {}
+    for name, c in sums.items():
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            f = c["FETCH_SIZE"][0] / c["FETCH_SIZE"][1]
+            w = c["WRITE_SIZE"][0] / c["WRITE_SIZE"][1]
+            out[name] = int(round((2 * f + w) * 1024))
+    return out
+
+
+def pmc_traffic(args, variant: int, mode: int, timeout_s: float = 180.0) -> dict:
+    """HBM bytes per launch of every kernel of the iteration, from two
+    rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE: one counter group per
+    run, kernel dispatch counters only) of a short child run of this same
+    workload with the same SpMV variant and iteration mode. FETCH_SIZE is
+    doubled (gfx950 tallies 128-B requests at 64 B; MI355X_MICROARCH.md,
+    HBM/rocprofv3 section); KB = 1024 B. The child starts as a new process
+    (this one has initialised the GPU: no exec), in its own process group,
+    killed whole on timeout."""
+    import glob
+    import shutil
+    import signal
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
+             "--steps", "10", "--warmup", "2", "--profile-steps", "0", "--no-cpu",
+             "--no-general", "--no-traffic", "--mode", str(mode), "--poll", str(args.poll)]
+    if args.grid:
+        child += ["--grid", str(args.grid)]
+    env = dict(os.environ, CGX_SPMV_VARIANT=str(variant))
+    env.pop("WORLD_SIZE", None)
+    sums: dict = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="cgx_pmc_")
+        try:
+            p = subprocess.Popen([prof, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv",
+                                  "--"] + child, env=env, stdout=subprocess.DEVNULL,
+                                 stderr=subprocess.PIPE, text=True, start_new_session=True)
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.communicate()
+                return {"error": f"rocprofv3 --pmc {ctr} timed out after {timeout_s:.0f} s"}
+            if p.returncode != 0:
+                return {"error": f"rocprofv3 --pmc {ctr} exited {p.returncode}: {err[-400:]}"}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                pmc_accumulate(open(f), ctr, sums)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return {"by_kernel": pmc_bytes(sums),
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate child runs of "
+                      "this workload, 2 + 10 bodies, same variant and mode), mean per dispatch; "
+                      "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE "
+                      "correction, MI355X_MICROARCH.md)"}
+
+
 def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
     """Solve a small slab problem (nxy x nxy x planes*world, `planes` z-planes
     per rank, b_i = i + 1, x0 = 0) twice on this node: over the device peer
@@ -509,13 +596,15 @@ def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
     rows = cga.DeviceArray(q, n_local + 1, np.int32)
     cols = cga.DeviceArray(q, nnz, np.int32)
     vals = cga.DeviceArray(q, nnz, np.float64)
-    check(L.cgx_poisson_fill(q.handle, F64, 3, nxy, nxy, nz, begin, begin + n_local, rows.ptr,
-                             cols.ptr, vals.ptr))
     b = cga.DeviceArray(q, n_local, np.float64)
     check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(begin)))
     out, xs = {}, {}
     why = None
     for name in ("peer", "setup"):
+        # cgx_csr_create_dist remaps the columns in place (global -> local +
+        # ghost numbering): every matrix gets freshly generated arrays
+        check(L.cgx_poisson_fill(q.handle, F64, 3, nxy, nxy, nz, begin, begin + n_local,
+                                 rows.ptr, cols.ptr, vals.ptr))
         A = C.c_void_p()
         check(L.cgx_csr_create_dist(q.handle, n_local * world, begin, n_local, nnz, rows.ptr,
                                     cols.ptr, vals.ptr, F64, C.byref(A)))

@@ -13,7 +13,8 @@ import bench  # noqa: E402
 
 def test_defaults_are_strong_scaling_of_256():
     a = bench.parse([])
-    assert a.gpus == 1 and a.grid == 256 and not a.weak and a.transport == "auto"
+    assert a.gpus == 1 and a.workload == "p3d_256" and a.grid is None and not a.weak
+    assert a.transport == "auto"
     assert bench.parse(["--weak"]).weak
 
 
@@ -69,3 +70,32 @@ def test_job_cores_reports_host():
     info = bench.job_cores()
     assert 1 <= info["use"] <= info["affinity"] <= (os.cpu_count() or info["affinity"])
     assert "model" in info and info["nproc"] == os.cpu_count()
+
+
+def test_pmc_csv_parsing():
+    """roofline.traffic: per-kernel (2 FETCH_SIZE + WRITE_SIZE) KB x 1024 from
+    rocprofv3 counter_collection.csv rows (the gfx950 FETCH correction)."""
+    import io
+    hdr = '"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+    fetch = io.StringIO(hdr +
+                        '1,"void cgx::k_spmv_dot<double, 1875970>(cgx::CsrArgs, double const*)",'
+                        '"FETCH_SIZE",100.0\n'
+                        '2,"void cgx::k_spmv_dot<double, 1875970>(cgx::CsrArgs, double const*)",'
+                        '"FETCH_SIZE",300.0\n'
+                        '3,"void cgx::(anonymous namespace)::k_poisson<double>(int)","FETCH_SIZE",7\n')
+    write = io.StringIO(hdr +
+                        '1,"void cgx::k_spmv_dot<double, 1875970>(cgx::CsrArgs, double const*)",'
+                        '"WRITE_SIZE",50.0\n')
+    sums = {}
+    bench.pmc_accumulate(fetch, "FETCH_SIZE", sums)
+    bench.pmc_accumulate(write, "WRITE_SIZE", sums)
+    out = bench.pmc_bytes(sums)
+    assert out == {"k_spmv_dot<double, 1875970>": (2 * 200 + 50) * 1024}
+    assert bench.kernel_base_name(
+        "void cgx::(anonymous namespace)::k_poisson<double>(int, int)") == "k_poisson<double>"
+
+
+def test_workload_choices():
+    for w in ("p3d_256", "p3d_512", "p2d_4096", "p2d_128", "g3_standin"):
+        assert bench.parse(["--workload", w]).workload == w
+    assert bench.parse([]).workload == "p3d_256" and bench.parse([]).grid is None

@@ -83,16 +83,19 @@ def _parse(stdout):
 def test_reference_tester_runs_on_gpu(name, exe):
     if not os.path.exists(exe):
         pytest.skip(f"{exe} not built (needs the reference sources at build time)")
+    # bytes, decoded without newline translation: the progress line's "\r"
+    # must survive (text=True would turn it into "\n")
     p = subprocess.run([exe, os.path.join(GOLD, name + ".mtx")], capture_output=True,
-                       text=True, timeout=120)
-    assert p.returncode == 0, p.stderr[-2000:]
-    n, nnz, ms, acc = _parse(p.stdout)
+                       timeout=120)
+    stdout, stderr = p.stdout.decode(), p.stderr.decode()
+    assert p.returncode == 0, stderr[-2000:]
+    n, nnz, ms, acc = _parse(stdout)
     g = np.load(os.path.join(GOLD, f"loader_{name}.npz"))
     assert n == len(g["rowptr"]) - 1 and nnz == len(g["val"])
     # Tester.cpp solves to 1e-24; accuracy() = ||b-Ax||^2/||x||^2 (Q6)
     gold = np.load(os.path.join(GOLD, f"cg_{name}.npz"))
     assert acc < 1e-24 and acc < 100 * float(gold["accuracy_1e-24"])
-    _check_verbose_trace(p.stderr, n, int(gold["iters_1e-24"]))
+    _check_verbose_trace(stderr, n, int(gold["iters_1e-24"]))
 
 
 # The std::clog sequence a Debuglevel::Verbose solver prints for Tester.cpp's
