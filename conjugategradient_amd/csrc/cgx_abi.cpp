@@ -534,6 +534,17 @@ extern "C" int cgx_create(int device, cgx_ctx **out) {
   if (e == hipSuccess) e = hipMemset(ctx->ws, 0, sizeof(RedWs<double>));
   if (e == hipSuccess) e = hipMalloc(&ctx->scratch, 64);
   if (e == hipSuccess) e = hipHostMalloc(&ctx->h_pinned, 1024, hipHostMallocDefault);
+  // the scalar state a standalone SpMV (cgx_spmv) runs k_spmv_dot with:
+  // slot 0 active, its p.Ap partials into ctx->ws (not read)
+  if (e == hipSuccess) e = hipMalloc(&ctx->spmv_st, sizeof(CgScalars<double>) + sizeof(CgScalars<float>));
+  if (e == hipSuccess) {
+    CgScalars<double> sd{};
+    CgScalars<float> sf{};
+    sd.active[0] = sf.active[0] = 1;
+    e = hipMemcpy(ctx->spmv_st, &sd, sizeof(sd), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy((char *)ctx->spmv_st + sizeof(sd), &sf, sizeof(sf), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     cgx_destroy(ctx);
     return hip_fail(e, "cgx_create");
@@ -572,6 +583,7 @@ static void ctx_free(cgx_ctx *ctx) {
   dist_comm_destroy(ctx);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->spmv_st) (void)hipFree(ctx->spmv_st);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
   for (int b = 0; b < 2; ++b) {
     if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
@@ -1460,8 +1472,7 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
 }
 
 static bool known_variant(int v) {
-  static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 64, 65, 66, 67,
-                           68, 69, 70, 71, 76, 77, 78, 79, 140, 141, 142, 143, 264, 265, 266,
+  static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
                            34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
                            821248, 821250, 1607680, 1607682, 1869824, 1869826};
@@ -1639,9 +1650,14 @@ extern "C" int cgx_spmv(cgx_ctx *ctx, cgx_csr *A, const void *x, void *y, int64_
   int rc = dist_extend(A, x, &xe);
   if (rc) return rc;
   if (A->dtype == CGX_F32)
-    CGX_HIP(Launch<float>::spmv(A->dev, (const float *)xe, (float *)y, ctx->stream));
+    CGX_HIP(Launch<float>::spmv(A->dev, (const float *)xe, (float *)y,
+                                (CgScalars<float> *)((char *)ctx->spmv_st +
+                                                     sizeof(CgScalars<double>)),
+                                (RedWs<float> *)ctx->ws, ctx->stream));
   else
-    CGX_HIP(Launch<double>::spmv(A->dev, (const double *)xe, (double *)y, ctx->stream));
+    CGX_HIP(Launch<double>::spmv(A->dev, (const double *)xe, (double *)y,
+                                 (CgScalars<double> *)ctx->spmv_st, (RedWs<double> *)ctx->ws,
+                                 ctx->stream));
   return CGX_OK;
 }
 
@@ -1783,6 +1799,10 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
               "4 fused with deferred x", mode);
   CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
               "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
+  CGX_REQUIRE(mode != 2 || (cg->dtype == CGX_F32 ? Launch<float>::fused_supported(cg->A->dev)
+                                                 : Launch<double>::fused_supported(cg->A->dev)),
+              CGX_EUNSUPPORTED, "mode 2 needs a production SpMV format (variant %d has no fused "
+              "kernel)", launch_variant(cg->A->dev, cg->dtype));
   CGX_REQUIRE(mode != 4 || (cg->dtype == CGX_F64 && Launch<double>::fd_supported(cg->A->dev)),
               CGX_EUNSUPPORTED, "mode 4 needs an f64 matrix in a production SpMV format "
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));

@@ -144,7 +144,10 @@ struct CsrDev {
 template <typename T> struct Launch {
   static int grid_rows(int nrb);
   static int grid_elems(int64_t n, int cap);
-  static hipError_t spmv(const CsrDev &A, const T *x, T *y, hipStream_t s);
+  // y = A x by k_spmv_dot in A's variant (st: slot 0 active; its p.Ap
+  // partials land in ws, unread): the standalone SpMV runs the loop's kernel
+  static hipError_t spmv(const CsrDev &A, const T *x, T *y, CgScalars<T> *st, RedWs<T> *ws,
+                         hipStream_t s);
   static hipError_t cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                             CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
                             hipStream_t s);
@@ -188,6 +191,7 @@ template <typename T> struct Launch {
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);
+  static bool fused_supported(const CsrDev &A);  // mode 2 (production forms)
   static hipError_t spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
                                CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s);
   static hipError_t flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,

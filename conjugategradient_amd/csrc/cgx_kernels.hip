@@ -661,134 +661,6 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
   }
 }
 
-// Three-stage software pipeline (variant bit 128, paired loads): while the
-// current block b is multiplied, staged and summed, the gathers and values of
-// block b+1 and the column indices of block b+2 are in flight, so each
-// memory latency (HBM for val/col, L2 for the gathers) gets a whole block's
-// time to resolve instead of lying on the block's critical path. Loads are
-// issued unconditionally (clamped to valid addresses); the row epilogue's own
-// loads go out before the prefetches (vmcnt counts in issue order).
-template <typename T, int V, class Epi, class Gather>
-__device__ __forceinline__ void spmv_rows_deep(const CsrArgs &A, const T *__restrict__ val,
-                                               const Gather &x, Epi &epi,
-                                               SpmvLds<T, TileOf<V>::tile> &sm) {
-  using TL = TileOf<V>;
-  constexpr bool NT = (V & 2) != 0;
-  using PV = typename PairOf<T>::V;
-  constexpr int U = TL::tile / (2 * kBlock);
-  const int t = threadIdx.x;
-  int b, step, end;
-  work_range<V>(A.nrb, b, step, end);
-  if (b >= end) return;
-  // pair window [ka, ka + 2*np) of a block's entries [k0, k1)
-  auto window = [](int kk0, int kk1, int &ka, int &np) {
-    const bool ok = kk1 > kk0;  // empty blocks read pairs [0, 1] (nnz >= 2)
-    ka = ok ? (kk0 & ~1) : 0;
-    np = ok ? ((kk1 - ka + 1) >> 1) : 1;
-  };
-  auto load_c = [&](int kk0, int kk1, Int2(&cc)[U]) {
-    int ka, np;
-    window(kk0, kk1, ka, np);
-    const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(t + u * kBlock, np - 1);
-      cc[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, kk1);
-    }
-  };
-  auto load_v = [&](int kk0, int kk1, PV(&vv)[U]) {
-    int ka, np;
-    window(kk0, kk1, ka, np);
-    const PV *v2 = reinterpret_cast<const PV *>(val + ka);
-#pragma unroll
-    for (int u = 0; u < U; ++u) vv[u] = ldg<NT>(v2 + min(t + u * kBlock, np - 1));
-  };
-  auto gather = [&](const Int2(&cc)[U], T(&g0)[U], T(&g1)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      g0[u] = x(cc[u].x);
-      g1[u] = x(cc[u].y);
-    }
-  };
-  // blocks b (current), b1 = b + step, b2 = b + 2 step (clamped to the last)
-  int b1 = b + step < end ? b + step : b;
-  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
-  int k0n = A.rbk[b1], k1n = A.rbk[b1 + 1];
-  Int2 cN[U];
-  PV vC[U];
-  T gC0[U], gC1[U];
-  load_c(k0, k1, cN);
-  gather(cN, gC0, gC1);  // waits for block b's columns (prologue only)
-  load_v(k0, k1, vC);
-  load_c(k0n, k1n, cN);
-  for (;;) {
-    const int nb = b + step;
-    const bool has_next = nb < end;
-    const int b2 = b1 + step < end ? b1 + step : b1;
-    const int k0nn = A.rbk[b2], k1nn = A.rbk[b2 + 1];
-    const int nrows = r1 - r0, cnt = k1 - k0;
-    // this block's row operands (issued before the next stages' loads)
-    const int tr = min(t, max(nrows - 1, 0));
-    const int a = A.rowptr[r0 + tr] - k0, e = A.rowptr[r0 + tr + 1] - k0;
-    epi.pre(r0 + tr);
-    __builtin_amdgcn_sched_barrier(0);
-    // stage 3 for b: products -> LDS (branch-free); vC / gC die here, so
-    // the next stages' registers reuse them (peak ~ one block in flight)
-    {
-      const int ka = k0 & ~1;
-      const int lim = min(cnt, TL::cap);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int pos = 2 * (t + u * kBlock) + ka - k0;
-        const int q0 = (pos >= 0 && pos < lim) ? pos : TL::tile;
-        const int q1 = (pos + 1 >= 0 && pos + 1 < lim) ? pos + 1 : TL::tile + 1;
-        sm.prod[q0] = vC[u].x * gC0[u];
-        sm.prod[q1] = vC[u].y * gC1[u];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // stage 2 for b1: gathers + values; stage 1 for b2: column indices
-    gather(cN, gC0, gC1);
-    load_v(k0n, k1n, vC);
-    __builtin_amdgcn_sched_barrier(0);
-    load_c(k0nn, k1nn, cN);
-    __builtin_amdgcn_sched_barrier(0);
-    if (cnt <= TL::cap) {
-      __syncthreads();
-      if (t < nrows) {
-        T s = T(0);
-        for (int j = a; j < e; ++j) s += sm.prod[j];
-        epi.row(r0 + t, s);
-      }
-      __syncthreads();
-    } else {
-      // one row longer than a tile
-      __syncthreads();
-      T s[1] = {T(0)};
-      for (int k = t; k < cnt; k += kBlock) s[0] += val[k0 + k] * x(A.col[k0 + k]);
-      block_sum<T, 1>(s, sm.red);
-      if (t == 0) epi.row(r0, s[0]);
-      __syncthreads();
-    }
-    if (!has_next) break;
-    b = nb;
-    r0 = A.rb[b];
-    r1 = A.rb[b + 1];
-    k0 = k0n;
-    k1 = k1n;
-    b1 = b2;
-    k0n = k0nn;
-    k1n = k1nn;
-  }
-}
-
-// Quad form of the pipelined loop (variant bit 256): the vector-memory
-// pipeline (TA/TD) is the measured bottleneck (profiles/r01_pmc_spmv.txt:
-// TA_TA_BUSY ~90 % of kernel cycles), so this form issues fewer memory
-// instructions per row block: val as two 16-B loads and col as one 16-B load
-// per 4 entries (pairs: 16-B + 8-B per 2 entries), and one row-pointer load
-// per row (the next row's start comes through LDS, the block's end from the
-// schedule) instead of two.
 template <typename T> struct QuadOf;
 template <> struct QuadOf<double> { typedef double V __attribute__((ext_vector_type(4))); };
 template <> struct QuadOf<float> { typedef float V __attribute__((ext_vector_type(4))); };
@@ -885,120 +757,6 @@ __device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__rest
       block_sum<T, 1>(s, sm.red);
       if (t == 0) epi.row(r0, s[0]);
       __syncthreads();
-    }
-    if (!has_next) break;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      v[u] = vn[u];
-      c[u] = cn[u];
-    }
-    b = nb;
-    r0 = nr0;
-    r1 = nr1;
-    k0 = nk0;
-    k1 = nk1;
-  }
-}
-
-// Wave tiles (variant bit 512): every wave owns its row blocks (<= 64 rows,
-// <= 506 entries; schedule tile 512), stages its products in its own LDS
-// slice and sums its rows without any workgroup barrier — LDS operations of
-// one wave complete in order, so a wave-level compiler fence is enough. Same
-// one-ahead pipeline as spmv_rows_pipe (paired loads). Rows longer than a
-// wave tile are summed by the whole wave (tree order).
-template <typename T> struct WaveLds {
-  T prod[4][512 + 4];  // per wave: tile + 4 scratch slots
-  T red[4 * kMaxRed];
-  int flag;
-  int rp[1];  // unused (keeps the SpmvLds member set)
-};
-
-template <typename T, int V, class Epi, class Gather>
-__device__ __forceinline__ void spmv_waves(const CsrArgs &A, const T *__restrict__ val,
-                                           const Gather &x, Epi &epi, WaveLds<T> &sm) {
-  constexpr bool NT = (V & 2) != 0;
-  using PV = typename PairOf<T>::V;
-  constexpr int WT = 512, CAP = WT - 6, U = WT / (2 * 64);
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  T *prod = sm.prod[w];
-  const int G = gridDim.x;
-  int b, step, end;
-  if ((V & 1) && (G & 7) == 0) {
-    const int g = blockIdx.x & 7;
-    b = (int)(((int64_t)A.nrb * g) >> 3) + (blockIdx.x >> 3) * 4 + w;
-    end = (int)(((int64_t)A.nrb * (g + 1)) >> 3);
-    step = (G >> 3) * 4;
-  } else {
-    b = blockIdx.x * 4 + w;
-    step = G * 4;
-    end = A.nrb;
-  }
-  if (b >= end) return;
-  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
-  PV v[U];
-  Int2 c[U];
-  auto issue = [&](int kk0, int kk1, PV(&vv)[U], Int2(&cc)[U]) {
-    const bool ok = kk1 > kk0;
-    const int ka = ok ? (kk0 & ~1) : 0;
-    const int np = ok ? ((kk1 - ka + 1) >> 1) : 1;
-    const PV *v2 = reinterpret_cast<const PV *>(val + ka);
-    const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(lane + u * 64, np - 1);
-      vv[u] = ldg<NT>(v2 + j);
-      cc[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, kk1);
-    }
-  };
-  issue(k0, k1, v, c);
-  for (;;) {
-    const int nb = b + step;
-    const bool has_next = nb < end;
-    const int nbb = has_next ? nb : b;
-    const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
-    const int nrows = r1 - r0, cnt = k1 - k0;
-    const int tr = min(lane, max(nrows - 1, 0));
-    const int rpt = A.rowptr[r0 + tr];
-    epi.pre(r0 + tr);
-    T g0[U], g1[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      g0[u] = x(c[u].x);
-      g1[u] = x(c[u].y);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    PV vn[U];
-    Int2 cn[U];
-    issue(nk0, nk1, vn, cn);
-    __builtin_amdgcn_sched_barrier(0);
-    if (cnt <= CAP) {
-      const int ka = k0 & ~1;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int pos = 2 * (lane + u * 64) + ka - k0;
-        const int q0 = (pos >= 0 && pos < cnt) ? pos : WT;
-        const int q1 = (pos + 1 >= 0 && pos + 1 < cnt) ? pos + 1 : WT + 1;
-        prod[q0] = v[u].x * g0[u];
-        prod[q1] = v[u].y * g1[u];
-      }
-      // end of row `lane`: the next lane's start, or the block's end
-      const int nxt = __shfl_down(rpt, 1, 64);
-      const int rend = (lane + 1 < nrows) ? nxt : k1;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      if (lane < nrows) {
-        T s = T(0);
-        for (int j = rpt - k0; j < rend - k0; ++j) s += prod[j];
-        epi.row(r0 + lane, s);
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else {
-      // one row longer than a wave tile: the whole wave sums it
-      T s = T(0);
-      for (int kk = lane; kk < cnt; kk += 64) s += val[k0 + kk] * x(A.col[k0 + kk]);
-      s = wave_sum(s);
-      if (lane == 0) epi.row(r0, s);
     }
     if (!has_next) break;
 #pragma unroll
@@ -1845,7 +1603,7 @@ template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::
 template <typename T, int V>
 using LdsOf = typename std::conditional<
     (V & (2048 | 8192)) != 0, SellLds<T>,
-    typename std::conditional<(V & 512) != 0, WaveLds<T>, SpmvLds<T, TileOf<V>::tile>>::type>::type;
+    SpmvLds<T, TileOf<V>::tile>>::type;
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
@@ -1855,9 +1613,7 @@ __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__
   else if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0) spmv_sell<T, V, Epi, Gather>(A, x, epi);
-  else if constexpr ((V & 512) != 0) spmv_waves<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 256) != 0) spmv_rows_quad<T, V, Epi, Gather>(A, val, x, epi, sm);
-  else if constexpr ((V & 128) != 0) spmv_rows_deep<T, V, Epi, Gather>(A, val, x, epi, sm);
   else if constexpr ((V & 8) != 0) spmv_rows_pipe<T, V, Epi, Gather>(A, val, x, epi, sm);
   else spmv_rows<T, V, Epi, Gather>(A, val, x, epi, sm);
 }
@@ -1871,17 +1627,6 @@ __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__
 // two rows, c0 = x[i0], c1 = x[i1], are already in registers (the
 // value-code kernel's center pair); only EpiDot, whose p IS the gathered
 // vector (k_spmv_dot), uses them.
-template <typename T> struct EpiStore {
-  T *__restrict__ y;
-  __device__ __forceinline__ void pre(int) {}
-  __device__ __forceinline__ void pre2c(int, int, T, T) {}
-  __device__ __forceinline__ void row(int i, T s) { y[i] = s; }
-  __device__ __forceinline__ void pre2(int, int) {}
-  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
-    if (l0) y[i] = s0;
-    if (l1) y[i + 1] = s1;
-  }
-};
 template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
   T *__restrict__ Ap;
   const T *__restrict__ p;
@@ -2072,14 +1817,6 @@ template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
     }
   }
 };
-
-template <typename T, int V>
-__global__ __launch_bounds__(kBlock) void k_spmv(CsrArgs A, const T *__restrict__ val,
-                                                 const T *__restrict__ x, T *__restrict__ y) {
-  __shared__ LdsOf<T, V> sm;
-  EpiStore<T> e{y};
-  spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
-}
 
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restrict__ val,
@@ -3145,20 +2882,18 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     v = -1;  // no SELL copy: CSR-stream
   }
   if (v < 0) v = (A.nnz * int64_t(sizeof(T) + sizeof(int)) >= kNtMinBytes) ? 15 : 13;
-  v &= 1023;  // bits 16/32: timing ablations, only reachable through cgx_tune_spmv
-  const int tile = A.tile == 1024 ? 64 : 0;  // the kernel tile follows the schedule
+  // bits 16/32: timing ablations, only reachable through cgx_tune_spmv; the
+  // retired half-tile (64), three-stage (128) and wave-tile (512) bits drop
+  // (a schedule built for smaller tiles fits the full-tile kernels)
+  v &= 1023 & ~(64 | 128 | 512);
   if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2)
-    return tile;  // plain loads, no pipelining (any schedule with <= 2042-entry blocks)
-  if (A.tile == 512) return 512 | 12 | (v & 3);  // wave tiles: 524..527
-  v &= ~512;
+    return 0;  // plain loads, no pipelining (any schedule with <= 2042-entry blocks)
   if ((v & 256) && (((uintptr_t)A.val % (4 * sizeof(T))) || ((uintptr_t)A.col % 16) ||
-                    A.nnz < 4 || tile))
-    v &= ~256;  // quads need 4-entry alignment and full tiles
+                    A.nnz < 4))
+    v &= ~256;  // quads need 4-entry alignment
   if (v & 256) return 256 | 8 | (v & 3);  // 264..267
   if ((v & 8) && !(v & 4)) v &= ~8;  // the pipelined loop uses paired loads
-  if ((v & 128) && (!(v & 4) || tile)) v &= ~128;  // deep pipeline: paired, full tiles
-  if (v & 128) v |= 8;
-  return v | tile;
+  return v;
 }
 
 #define CGX_LAUNCH_V(KERNEL, VV, ...)                                          \
@@ -3168,71 +2903,60 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     return hipGetLastError();                                                  \
   } while (0)
 
-#define CGX_SPMV_SWITCH(v, KERNEL, ...)                                        \
-  switch (v) {                                                                 \
-    case 0: CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);                                      \
-    case 1: CGX_LAUNCH_V(KERNEL, 1, __VA_ARGS__);                                      \
-    case 2: CGX_LAUNCH_V(KERNEL, 2, __VA_ARGS__);                                      \
-    case 3: CGX_LAUNCH_V(KERNEL, 3, __VA_ARGS__);                                      \
-    case 4: CGX_LAUNCH_V(KERNEL, 4, __VA_ARGS__);                                      \
-    case 5: CGX_LAUNCH_V(KERNEL, 5, __VA_ARGS__);                                      \
-    case 6: CGX_LAUNCH_V(KERNEL, 6, __VA_ARGS__);                                      \
-    case 7: CGX_LAUNCH_V(KERNEL, 7, __VA_ARGS__);                                      \
-    case 12: CGX_LAUNCH_V(KERNEL, 12, __VA_ARGS__);                                    \
-    case 13: CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);                                    \
-    case 14: CGX_LAUNCH_V(KERNEL, 14, __VA_ARGS__);                                    \
-    case 15: CGX_LAUNCH_V(KERNEL, 15, __VA_ARGS__);                                    \
-    case 64: CGX_LAUNCH_V(KERNEL, 64, __VA_ARGS__);                                    \
-    case 65: CGX_LAUNCH_V(KERNEL, 65, __VA_ARGS__);                                    \
-    case 66: CGX_LAUNCH_V(KERNEL, 66, __VA_ARGS__);                                    \
-    case 67: CGX_LAUNCH_V(KERNEL, 67, __VA_ARGS__);                                    \
-    case 68: CGX_LAUNCH_V(KERNEL, 68, __VA_ARGS__);                                    \
-    case 69: CGX_LAUNCH_V(KERNEL, 69, __VA_ARGS__);                                    \
-    case 70: CGX_LAUNCH_V(KERNEL, 70, __VA_ARGS__);                                    \
-    case 71: CGX_LAUNCH_V(KERNEL, 71, __VA_ARGS__);                                    \
-    case 524: CGX_LAUNCH_V(KERNEL, 524, __VA_ARGS__);                                 \
-    case 525: CGX_LAUNCH_V(KERNEL, 525, __VA_ARGS__);                                 \
-    case 526: CGX_LAUNCH_V(KERNEL, 526, __VA_ARGS__);                                 \
-    case 527: CGX_LAUNCH_V(KERNEL, 527, __VA_ARGS__);                                 \
-    case 264: CGX_LAUNCH_V(KERNEL, 264, __VA_ARGS__);                                 \
-    case 265: CGX_LAUNCH_V(KERNEL, 265, __VA_ARGS__);                                 \
-    case 266: CGX_LAUNCH_V(KERNEL, 266, __VA_ARGS__);                                 \
-    case 267: CGX_LAUNCH_V(KERNEL, 267, __VA_ARGS__);                                 \
-    case 140: CGX_LAUNCH_V(KERNEL, 140, __VA_ARGS__);                                 \
-    case 141: CGX_LAUNCH_V(KERNEL, 141, __VA_ARGS__);                                 \
-    case 142: CGX_LAUNCH_V(KERNEL, 142, __VA_ARGS__);                                 \
-    case 143: CGX_LAUNCH_V(KERNEL, 143, __VA_ARGS__);                                 \
-    case 76: CGX_LAUNCH_V(KERNEL, 76, __VA_ARGS__);                                    \
-    case 77: CGX_LAUNCH_V(KERNEL, 77, __VA_ARGS__);                                    \
-    case 78: CGX_LAUNCH_V(KERNEL, 78, __VA_ARGS__);                                    \
-    case 79: CGX_LAUNCH_V(KERNEL, 79, __VA_ARGS__);                                    \
-    case 2048: CGX_LAUNCH_V(KERNEL, 2048, __VA_ARGS__);                               \
-    case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);                               \
-    case 2056: CGX_LAUNCH_V(KERNEL, 2056, __VA_ARGS__);                               \
-    case 2058: CGX_LAUNCH_V(KERNEL, 2058, __VA_ARGS__);                               \
-    case 6144: CGX_LAUNCH_V(KERNEL, 6144, __VA_ARGS__);                               \
-    case 6146: CGX_LAUNCH_V(KERNEL, 6146, __VA_ARGS__);                               \
-    case 8192: CGX_LAUNCH_V(KERNEL, 8192, __VA_ARGS__);                               \
-    case 8194: CGX_LAUNCH_V(KERNEL, 8194, __VA_ARGS__);                               \
-    case 24576: CGX_LAUNCH_V(KERNEL, 24576, __VA_ARGS__);                             \
-    case 24578: CGX_LAUNCH_V(KERNEL, 24578, __VA_ARGS__);                             \
-    case 40960: CGX_LAUNCH_V(KERNEL, 40960, __VA_ARGS__);                             \
-    case 40962: CGX_LAUNCH_V(KERNEL, 40962, __VA_ARGS__);                             \
-    case 303104: CGX_LAUNCH_V(KERNEL, 303104, __VA_ARGS__);                           \
-    case 303106: CGX_LAUNCH_V(KERNEL, 303106, __VA_ARGS__);                           \
-    case 565248: CGX_LAUNCH_V(KERNEL, 565248, __VA_ARGS__);                           \
-    case 565250: CGX_LAUNCH_V(KERNEL, 565250, __VA_ARGS__);                           \
-    case 827392: CGX_LAUNCH_V(KERNEL, 827392, __VA_ARGS__);                           \
-    case 827394: CGX_LAUNCH_V(KERNEL, 827394, __VA_ARGS__);                           \
-    case 1613824: CGX_LAUNCH_V(KERNEL, 1613824, __VA_ARGS__);                         \
-    case 1613826: CGX_LAUNCH_V(KERNEL, 1613826, __VA_ARGS__);                         \
-    case 1875968: CGX_LAUNCH_V(KERNEL, 1875968, __VA_ARGS__);                         \
-    case 1875970: CGX_LAUNCH_V(KERNEL, 1875970, __VA_ARGS__);                         \
-    case 3710976: CGX_LAUNCH_V(KERNEL, 3710976, __VA_ARGS__);                         \
-    case 3710978: CGX_LAUNCH_V(KERNEL, 3710978, __VA_ARGS__);                         \
-    case 3973120: CGX_LAUNCH_V(KERNEL, 3973120, __VA_ARGS__);                         \
-    case 3973122: CGX_LAUNCH_V(KERNEL, 3973122, __VA_ARGS__);                         \
-    default: return hipErrorInvalidValue;                                      \
+// The SpMV forms k_spmv_dot is instantiated for (and cgx_csr_set_variant
+// accepts, cgx_abi.cpp known_variant): CSR-stream 0-7 (bits 1 XCD split, 2
+// non-temporal, 4 paired loads), 12-15 (+8 pipelined), 264-267 (quads);
+// dictionary SELL 2048/2050/2056/2058/6144/6146; SELL-P 8192/8194 (+16384:
+// 24576/24578); value-code SELL-P and its pipelined / stencil / plane-march
+// loops. (Round 1's half-tile, three-stage and wave-tile CSR forms, negative
+// results recorded in DESIGN.md §8, were retired in round 3.) One-off
+// kernels (cg init, accuracy) run CSR-stream: every form gives the same
+// per-row sums.
+#define CGX_SPMV_SWITCH(v, KERNEL, ...)                        \
+  switch (v) {                                                 \
+    case 0: CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);              \
+    case 1: CGX_LAUNCH_V(KERNEL, 1, __VA_ARGS__);              \
+    case 2: CGX_LAUNCH_V(KERNEL, 2, __VA_ARGS__);              \
+    case 3: CGX_LAUNCH_V(KERNEL, 3, __VA_ARGS__);              \
+    case 4: CGX_LAUNCH_V(KERNEL, 4, __VA_ARGS__);              \
+    case 5: CGX_LAUNCH_V(KERNEL, 5, __VA_ARGS__);              \
+    case 6: CGX_LAUNCH_V(KERNEL, 6, __VA_ARGS__);              \
+    case 7: CGX_LAUNCH_V(KERNEL, 7, __VA_ARGS__);              \
+    case 12: CGX_LAUNCH_V(KERNEL, 12, __VA_ARGS__);            \
+    case 13: CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);            \
+    case 14: CGX_LAUNCH_V(KERNEL, 14, __VA_ARGS__);            \
+    case 15: CGX_LAUNCH_V(KERNEL, 15, __VA_ARGS__);            \
+    case 264: CGX_LAUNCH_V(KERNEL, 264, __VA_ARGS__);          \
+    case 265: CGX_LAUNCH_V(KERNEL, 265, __VA_ARGS__);          \
+    case 266: CGX_LAUNCH_V(KERNEL, 266, __VA_ARGS__);          \
+    case 267: CGX_LAUNCH_V(KERNEL, 267, __VA_ARGS__);          \
+    case 2048: CGX_LAUNCH_V(KERNEL, 2048, __VA_ARGS__);        \
+    case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);        \
+    case 2056: CGX_LAUNCH_V(KERNEL, 2056, __VA_ARGS__);        \
+    case 2058: CGX_LAUNCH_V(KERNEL, 2058, __VA_ARGS__);        \
+    case 6144: CGX_LAUNCH_V(KERNEL, 6144, __VA_ARGS__);        \
+    case 6146: CGX_LAUNCH_V(KERNEL, 6146, __VA_ARGS__);        \
+    case 8192: CGX_LAUNCH_V(KERNEL, 8192, __VA_ARGS__);        \
+    case 8194: CGX_LAUNCH_V(KERNEL, 8194, __VA_ARGS__);        \
+    case 24576: CGX_LAUNCH_V(KERNEL, 24576, __VA_ARGS__);      \
+    case 24578: CGX_LAUNCH_V(KERNEL, 24578, __VA_ARGS__);      \
+    case 40960: CGX_LAUNCH_V(KERNEL, 40960, __VA_ARGS__);      \
+    case 40962: CGX_LAUNCH_V(KERNEL, 40962, __VA_ARGS__);      \
+    case 303104: CGX_LAUNCH_V(KERNEL, 303104, __VA_ARGS__);    \
+    case 303106: CGX_LAUNCH_V(KERNEL, 303106, __VA_ARGS__);    \
+    case 565248: CGX_LAUNCH_V(KERNEL, 565248, __VA_ARGS__);    \
+    case 565250: CGX_LAUNCH_V(KERNEL, 565250, __VA_ARGS__);    \
+    case 827392: CGX_LAUNCH_V(KERNEL, 827392, __VA_ARGS__);    \
+    case 827394: CGX_LAUNCH_V(KERNEL, 827394, __VA_ARGS__);    \
+    case 1613824: CGX_LAUNCH_V(KERNEL, 1613824, __VA_ARGS__);  \
+    case 1613826: CGX_LAUNCH_V(KERNEL, 1613826, __VA_ARGS__);  \
+    case 1875968: CGX_LAUNCH_V(KERNEL, 1875968, __VA_ARGS__);  \
+    case 1875970: CGX_LAUNCH_V(KERNEL, 1875970, __VA_ARGS__);  \
+    case 3710976: CGX_LAUNCH_V(KERNEL, 3710976, __VA_ARGS__);  \
+    case 3710978: CGX_LAUNCH_V(KERNEL, 3710978, __VA_ARGS__);  \
+    case 3973120: CGX_LAUNCH_V(KERNEL, 3973120, __VA_ARGS__);  \
+    case 3973122: CGX_LAUNCH_V(KERNEL, 3973122, __VA_ARGS__);  \
+    default: return hipErrorInvalidValue;                      \
   }
 
 // Workgroups of k_spmv_dot<T, v> resident on the device at once (occupancy
@@ -3241,14 +2965,12 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 // after the first ones finish their fixed shares, and that tail measured
 // 8% of the value-code kernel at 256^3 (tools/gpu_vc_ab.sh). $CGX_SPMV_RESIDENT=0
 // turns the cap off (A/B).
-#define CGX_SPMV_LIST(X)                                                              \
-  X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(64) X(65) X(66)   \
-  X(67) X(68) X(69) X(70) X(71) X(524) X(525) X(526) X(527) X(264) X(265) X(266)      \
-  X(267) X(140) X(141) X(142) X(143) X(76) X(77) X(78) X(79) X(2048) X(2050) X(2056)  \
-  X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)        \
-  X(40978) X(106498) X(172034) X(303104) X(303106) X(303122) X(827392) X(827394)        \
-  X(827410) X(565248) X(565250) X(1613824) X(1613826) X(1875968) X(1875970) \
-  X(3710976) X(3710978) X(3973120) X(3973122)
+#define CGX_SPMV_LIST(X)                                                                    \
+  X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(264) X(265) X(266)      \
+  X(267) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578)  \
+  X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
+  X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122) X(40978)     \
+  X(106498) X(172034) X(303122) X(827410)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \
@@ -3288,18 +3010,30 @@ template <typename T> static int cap_resident(int grid, int v) {
   return (r > 0 && r < grid) ? r : grid;
 }
 
+// The standalone SpMV (VectorOperations::spmv, cgx_spmv) is the loop's
+// k_spmv_dot in the matrix's variant, slot 0 of a context state that is
+// always active; its p.Ap partials land in ws and are not read.
 template <typename T>
-hipError_t Launch<T>::spmv(const CsrDev &A, const T *x, T *y, hipStream_t s) {
-  const int spmv_grid_ = grid_rows(A.nrb);
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv, args(A), (const T *)A.val, x, y);
+hipError_t Launch<T>::spmv(const CsrDev &A, const T *x, T *y, CgScalars<T> *st, RedWs<T> *ws,
+                           hipStream_t s) {
+  return spmv_dot(A, x, y, st, 0, ws, s, 0);
 }
+// One-off SpMV kernels (the init r = b - A x, accuracy()) run CSR-stream on
+// the caller's CSR arrays, whatever the loop's form: every form computes the
+// same per-row sums, and one launch per solve does not pay for an
+// instantiation per form. 13: pipelined paired loads (0 when val / col are
+// not aligned for them).
+#define CGX_CSR_ONEOFF(KERNEL, ...)                                             \
+  do {                                                                          \
+    const int spmv_grid_ = grid_rows(A.nrb);                                    \
+    if (spmv_variant<T>(A, 13) == 13) CGX_LAUNCH_V(KERNEL, 13, __VA_ARGS__);    \
+    CGX_LAUNCH_V(KERNEL, 0, __VA_ARGS__);                                       \
+  } while (0)
 template <typename T>
 hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *p,
                               CgScalars<T> *st, RedWs<T> *ws, T tol, long long cap,
                               hipStream_t s) {
-  const int spmv_grid_ = grid_rows(A.nrb);
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws,
-                  tol, cap);
+  CGX_CSR_ONEOFF(k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws, tol, cap);
 }
 template <typename T>
 hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
@@ -3387,6 +3121,12 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
   X(13) X(15) X(8192) X(8194) X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) \
   X(827392) X(827394) X(1613824) X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) \
   X(3973120) X(3973122)
+
+// mode 2 (k_spmv_fused): mode 4's forms, plain CSR-stream and the
+// dictionary SELL forms small matrices take
+#define CGX_FUSED_LIST(X)                                                                \
+  CGX_FD_LIST(X) X(0) X(5) X(265) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(24576) \
+  X(24578)
 
 template <typename T> static const void *spmv_fd_kernel(int v) {
   if constexpr (!std::is_same<T, double>::value) {
@@ -3524,8 +3264,23 @@ template <typename T>
 hipError_t Launch<T>::spmv_fused(const CsrDev &A, const T *r, const T *pp, T *pc, T *x, T *Ap,
                                  CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s) {
   const int spmv_grid_ = grid_rows(A.nrb);
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_spmv_fused, args(A), (const T *)A.val, r, pp, pc, x, Ap,
-                  st, slot, ws);
+  switch (spmv_variant<T>(A)) {  // mode 4's forms and the small-matrix ones
+#define CGX_KFU(VV)                                                                   \
+  case VV:                                                                            \
+    CGX_LAUNCH_V(k_spmv_fused, VV, args(A), (const T *)A.val, r, pp, pc, x, Ap, st, slot, ws);
+    CGX_FUSED_LIST(CGX_KFU)
+#undef CGX_KFU
+    default: return hipErrorInvalidValue;
+  }
+}
+template <typename T> bool Launch<T>::fused_supported(const CsrDev &A) {
+  switch (spmv_variant<T>(A)) {
+#define CGX_KFS(VV) case VV:
+    CGX_FUSED_LIST(CGX_KFS)
+#undef CGX_KFS
+    return true;
+    default: return false;
+  }
 }
 template <typename T>
 hipError_t Launch<T>::flush_x(int64_t n, T *x, const T *p, CgScalars<T> *st, int slot,
@@ -3598,8 +3353,7 @@ hipError_t Launch<T>::iota(T *d, int64_t n, double offset, hipStream_t s) {
 template <typename T>
 hipError_t Launch<T>::accuracy(const CsrDev &A, const T *b, const T *x, T *out2,
                                RedWs<T> *ws, hipStream_t s) {
-  const int spmv_grid_ = grid_rows(A.nrb);
-  CGX_SPMV_SWITCH(spmv_variant<T>(A), k_accuracy, args(A), (const T *)A.val, b, x, out2, ws);
+  CGX_CSR_ONEOFF(k_accuracy, args(A), (const T *)A.val, b, x, out2, ws);
 }
 template <typename T>
 hipError_t Launch<T>::poisson(int dim, int nx, int ny, int nz, int64_t row_begin,

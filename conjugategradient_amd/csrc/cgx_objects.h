@@ -123,6 +123,7 @@ struct cgx_ctx {
   hipStream_t stream = nullptr;
   void *ws = nullptr;           // cgx::RedWs<double> (large enough for float)
   void *scratch = nullptr;      // 2 doubles for accuracy() results
+  void *spmv_st = nullptr;      // CgScalars<double>, then <float>: slot 0 active (cgx_spmv)
   void *h_pinned = nullptr;     // pinned host staging (1 KiB: polls | host all-reduce)
   // pinned ring for large host<->device copies (cgx_h2d / cgx_d2h), lazily
   void *stage[2] = {nullptr, nullptr};
