@@ -335,6 +335,8 @@ def run(args) -> None:
     check(L.cgx_csr_variant(A, C.byref(variant)))
     sbytes = C.c_int64(0)
     check(L.cgx_csr_stream_bytes(A, C.byref(sbytes)))
+    ntpl, tpl_slices = C.c_int(0), C.c_int64(0)
+    check(L.cgx_csr_templates(A, C.byref(ntpl), C.byref(tpl_slices)))
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
@@ -482,7 +484,12 @@ def run(args) -> None:
                                      4: "2 kernels (p update in the SpMV), x update deferred "
                                         "over 4 bodies"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
-                       "spmv_variant": int(variant.value)},
+                       "spmv_variant": int(variant.value),
+                       "value_code_templates": (
+                           {"templates": ntpl.value, "slices": tpl_slices.value,
+                            "slices_total": (n_local + 127) // 128,
+                            "in_use": bool(variant.value & 8388608)}
+                           if ntpl.value else None)},
             "roofline": roof,
             "csr_general": general,
             "cpu_baseline": cpu,

@@ -18,6 +18,7 @@
 #include <tuple>
 #include <type_traits>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "cgx_objects.h"
@@ -886,7 +887,7 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
 void free_sell(cgx_csr *A) {
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
                    &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask, &A->d_sell_vc,
-                   &A->d_sell_vdict, &A->d_sell_vc4}) {
+                   &A->d_sell_vdict, &A->d_sell_vc4, &A->d_sell_sl_t, &A->d_vct}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
@@ -902,6 +903,10 @@ void free_sell(cgx_csr *A) {
   A->dev.svdict = nullptr;
   A->dev.nvdict = 0;
   A->dev.svc4 = nullptr;
+  A->dev.sl_t = nullptr;
+  A->dev.vct = nullptr;
+  A->dev.nvt = 0;
+  A->vt_slices = 0;
   A->split_ni = A->split_nb = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
@@ -1278,9 +1283,82 @@ template <typename T> static int build_value_codes_t(cgx_csr *A) {
   return CGX_OK;
 }
 
+// Value-code templates (cgx_internal.h kVT): the kVtMax most
+// frequent 4-bit code chunks that at least kVtMin slices share (hashes on
+// the device, counted here), and the template slice table in which every
+// slice whose chunk equals one of them byte for byte (checked on the
+// device) points at it. The matrix then also has the kVT forms; the
+// autotune decides. $CGX_VT=0 skips it. Errors are device failures only.
+static int build_value_templates(cgx_csr *A) {
+  constexpr int64_t kVtMin = 64;
+  if (!A->dev.svc4 || A->dev.sell_maxw > 8 || A->dev.nsl < kVtMin) return CGX_OK;
+  if (const char *env = std::getenv("CGX_VT"))
+    if (std::atoi(env) == 0) return CGX_OK;
+  hipStream_t s = A->ctx->stream;
+  const int64_t nsl = A->dev.nsl;
+  unsigned long long *dh = nullptr;
+  CGX_HIP(hipMalloc(&dh, (size_t)nsl * 8));
+  std::vector<unsigned long long> h((size_t)nsl);
+  hipError_t e = vc_hash(A->dev, dh, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h.data(), dh, (size_t)nsl * 8, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(dh);
+  if (e != hipSuccess) return hip_fail(e, "cgx_csr_create(template hashes)");
+  std::unordered_map<unsigned long long, std::pair<int64_t, int64_t>> cnt;  // count, first slice
+  for (int64_t q = 0; q < nsl; ++q)
+    if (h[q]) {
+      auto it = cnt.try_emplace(h[q], 0, q).first;
+      it->second.first += 1;
+    }
+  std::vector<std::pair<int64_t, int64_t>> top;  // (count, slice)
+  for (const auto &kv : cnt)
+    if (kv.second.first >= kVtMin) top.push_back(kv.second);
+  std::sort(top.begin(), top.end(), [](const auto &a, const auto &b) {
+    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  });
+  if (top.size() > (size_t)kVtMax) top.resize(kVtMax);
+  if (top.empty()) return CGX_OK;
+  const int nt = (int)top.size();
+  void *vct = nullptr, *slt = nullptr, *dcnt = nullptr;
+  e = hipMalloc(&vct, (size_t)nt * 64 * 8);
+  if (e == hipSuccess) e = hipMalloc(&slt, (size_t)nsl * sizeof(SellSlice));
+  if (e == hipSuccess) e = hipMalloc(&dcnt, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemsetAsync(dcnt, 0, sizeof(unsigned), s);
+  for (int t = 0; t < nt && e == hipSuccess; ++t) {  // template t: slice top[t]'s chunk
+    SellSlice m;
+    e = hipMemcpyAsync(&m, A->dev.sl + top[t].second, sizeof(m), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync((char *)vct + (size_t)t * 512,
+                         (const unsigned long long *)A->dev.svc4 + m.ioff, 512,
+                         hipMemcpyDeviceToDevice, s);
+  }
+  unsigned matched = 0;
+  if (e == hipSuccess)
+    e = vc_match(A->dev, (const unsigned long long *)vct, nt, (SellSlice *)slt, (unsigned *)dcnt, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(&matched, dcnt, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (dcnt) (void)hipFree(dcnt);
+  if (e != hipSuccess) {
+    if (vct) (void)hipFree(vct);
+    if (slt) (void)hipFree(slt);
+    return hip_fail(e, "cgx_csr_create(value-code templates)");
+  }
+  A->d_vct = vct;
+  A->d_sell_sl_t = slt;
+  A->dev.vct = vct;
+  A->dev.sl_t = (const SellSlice *)slt;
+  A->dev.nvt = nt;
+  A->vt_slices = matched;
+  return CGX_OK;
+}
+
 int build_value_codes(cgx_csr *A) {
   if (!A->dev.sl || !A->dev.sell_kind || A->dev.nsl < 1 || A->dev.nnz < 1) return CGX_OK;
-  return A->dtype == CGX_F32 ? build_value_codes_t<float>(A) : build_value_codes_t<double>(A);
+  const int rc =
+      A->dtype == CGX_F32 ? build_value_codes_t<float>(A) : build_value_codes_t<double>(A);
+  return rc ? rc : build_value_templates(A);
 }
 
 // SELL copy of A on the device with R rows per lane (0: the default layout),
@@ -1438,7 +1516,9 @@ extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
   const int v = launch_variant(A->dev, A->dtype);
   const int64_t es = (int64_t)dtype_size(A->dtype), nsl = A->dev.nsl;
   const int64_t desc = nsl * (int64_t)sizeof(SellSlice);
-  if (v & 32768)
+  if ((v & 32768) && (v & kVT))  // template slices read their chunk from LDS
+    *bytes = 8 * (A->vc_chunks - 64 * A->vt_slices) + desc + 512 * (int64_t)A->dev.nvt;
+  else if (v & 32768)
     *bytes = ((v & 262144) ? 8 : 16) * A->vc_chunks + desc;
   else if (v & 8192)
     *bytes = es * A->sell_padded + nsl * 2 * kSellRows * ((v & 16384) ? 4 : 1) + desc;
@@ -1452,6 +1532,13 @@ extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
 extern "C" int cgx_csr_value_codes(cgx_csr *A, int *n_values) {
   CGX_REQUIRE(A && n_values, CGX_EINVAL, "NULL argument");
   *n_values = A->dev.svc ? A->dev.nvdict : 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_templates(cgx_csr *A, int *n_templates, int64_t *slices) {
+  CGX_REQUIRE(A && n_templates && slices, CGX_EINVAL, "NULL argument");
+  *n_templates = A->dev.sl_t ? A->dev.nvt : 0;
+  *slices = A->dev.sl_t ? A->vt_slices : 0;
   return CGX_OK;
 }
 
@@ -1475,13 +1562,14 @@ static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
                            34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
-                           821248, 821250, 1607680, 1607682, 1869824, 1869826};
+                           821248, 821250, 1607680, 1607682, 1869824, 1869826,
+                           9209856, 9209858, 10258432, 10258434, 12355584, 12355586};
   for (int k : ok)
     if (k == v) return true;
   // the resolved SELL-P forms cgx_csr_variant reports (e.g. 1875970) are
   // accepted back as requests
   constexpr int sellp_bits =
-      8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2097152 | 2;
+      8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2097152 | kVT | 2;
   return (v & 8192) && !(v & ~sellp_bits);
 }
 
@@ -1494,6 +1582,8 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
               "variant %d needs SELL-P value codes, which this matrix does not have", variant);
   CGX_REQUIRE(!(variant & 262144) || A->dev.svc4, CGX_EUNSUPPORTED,
               "variant %d needs 4-bit value codes (at most 15 distinct values)", variant);
+  CGX_REQUIRE(!(variant & kVT) || A->dev.sl_t, CGX_EUNSUPPORTED,
+              "variant %d needs value-code templates, which this matrix does not have", variant);
   // the bit mask is not enough: check the form the request resolves to on
   // this matrix has a kernel (e.g. 2138112, plane march without the pipe
   // bits, has none)
@@ -1557,9 +1647,11 @@ int autotune_spmv(cgx_csr *A) {
   // 1048576: one gather pair fewer per offset -1 / +1)
   for (int c4 : {0, 262144}) {
     if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
-    for (int pipe : {0, 524288, 524288 | 1048576, 524288 | 1048576 | 2097152}) {
+    for (int pipe : {0, 524288, 524288 | 1048576, 524288 | 1048576 | 2097152,
+                     524288 | kVT, 524288 | 1048576 | kVT, 524288 | 1048576 | 2097152 | kVT}) {
       if (pipe && A->dev.sell_maxw > 8) continue;
       if ((pipe & 2097152) && A->dev.march_k < 1) continue;
+      if ((pipe & kVT) && (!c4 || !A->dev.sl_t)) continue;
       if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
       cands.push_back(2050 | 32768 | c4 | pipe);
     }
@@ -1587,16 +1679,20 @@ int autotune_spmv(cgx_csr *A) {
   for (int round = 0; round < 3 && e == hipSuccess; ++round) {
     for (size_t ci = 0; ci < cands.size() && e == hipSuccess; ++ci) {
       const int v = cands[ci];
+      // the candidate as the matrix's variant (the kernel arguments follow
+      // it: the kVT forms read the template slice table)
+      CsrDev dv = A->dev;
+      dv.variant = v;
       float tot = 0;
       for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
         if (rep == 1) e = hipEventRecord(e0, s);
         if (e != hipSuccess) break;
         if (A->dtype == CGX_F32)
-          e = Launch<float>::spmv_dot_variant(v, A->dev, (const float *)x, (float *)y,
+          e = Launch<float>::spmv_dot_variant(v, dv, (const float *)x, (float *)y,
                                               (CgScalars<float> *)st, (RedWs<float> *)ctx->ws,
                                               s);
         else
-          e = Launch<double>::spmv_dot_variant(v, A->dev, (const double *)x, (double *)y,
+          e = Launch<double>::spmv_dot_variant(v, dv, (const double *)x, (double *)y,
                                                (CgScalars<double> *)st,
                                                (RedWs<double> *)ctx->ws, s);
       }
@@ -1613,6 +1709,39 @@ int autotune_spmv(cgx_csr *A) {
       best = tbest[ci];
       best_v = cands[ci];
     }
+  // A 2-D plane-march winner runs the loop as mode 4 (fd_auto), i.e. as
+  // k_spmv_fd, whose register budget differs from k_spmv_dot's: with value-
+  // code templates it holds 3 waves per SIMD against 2 (152 against 169
+  // VGPRs) while k_spmv_dot loses one (profiles/r03_vt3.log: 4096^2 loop
+  // 95-99 against 103-104 us, isolated k_spmv_dot 58.6 against 54.2). The
+  // march and its template form are therefore decided on their fd kernels.
+  if (e == hipSuccess && A->dtype == CGX_F64 && (best_v & 2097152) && !(best_v & kVT) &&
+      A->dev.march_k > 0 && A->dev.march_a == 0 && A->dev.sl_t) {
+    const int pair[2] = {best_v, best_v | kVT};
+    float tf[2] = {1e30f, 1e30f};
+    void *ap = nullptr;
+    e = hipMalloc(&ap, nx * es);
+    const int npr = Launch<double>::update_parts(A->dev.n);
+    for (int round = 0; round < 3 && e == hipSuccess; ++round)
+      for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        CsrDev dv = A->dev;
+        dv.variant = pair[k];
+        float tot = 0;
+        for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
+          if (rep == 1) e = hipEventRecord(e0, s);
+          if (e == hipSuccess)
+            e = Launch<double>::spmv_fd(dv, (const double *)x, (const double *)x, (double *)y,
+                                        (double *)ap, (CgScalars<double> *)st, 0,
+                                        (RedWs<double> *)ctx->ws, npr, s);
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, s);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
+        if (e == hipSuccess) tf[k] = std::min(tf[k], tot);
+      }
+    if (ap) (void)hipFree(ap);
+    if (e == hipSuccess && tf[1] < tf[0]) best_v = pair[1];
+  }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   for (void *p : {x, y, st})
@@ -2219,14 +2348,16 @@ extern "C" int cgx_tune_spmv(cgx_ctx *ctx, cgx_csr *A, int variant, const void *
   CGX_HIP(hipEventCreate(&e0));
   CGX_HIP(hipEventCreate(&e1));
   hipError_t e = hipSuccess;
+  CsrDev dv = A->dev;  // the requested form as the matrix's (kVT: template slice table)
+  dv.variant = variant;
   for (int i = 0; i <= iters && e == hipSuccess; ++i) {  // first launch = warm-up
     if (i == 1) e = hipEventRecord(e0, s);
     if (e != hipSuccess) break;
     if (A->dtype == CGX_F32)
-      e = Launch<float>::spmv_dot_variant(variant, A->dev, (const float *)x, (float *)y,
+      e = Launch<float>::spmv_dot_variant(variant, dv, (const float *)x, (float *)y,
                                           (CgScalars<float> *)st, (RedWs<float> *)ctx->ws, s);
     else
-      e = Launch<double>::spmv_dot_variant(variant, A->dev, (const double *)x, (double *)y,
+      e = Launch<double>::spmv_dot_variant(variant, dv, (const double *)x, (double *)y,
                                            (CgScalars<double> *)st, (RedWs<double> *)ctx->ws, s);
   }
   if (e == hipSuccess) e = hipEventRecord(e1, s);

@@ -91,6 +91,16 @@ constexpr int kVcMax = 255;
 constexpr int kVcDict = 256;  // dictionary slots (entries past nvdict: zero)
 constexpr unsigned kVcAbsent = 0xff;
 constexpr int kVc4Max = 15;  // 4-bit codes: 15 values, 0xf empty
+// Value-code templates (variant bit kVT): the most frequent
+// 64-lane chunks of 4-bit codes (a constant-coefficient stencil has a
+// handful) are stored once, up to kVtMax of them, and copied into every
+// workgroup's LDS; a slice whose chunk equals template t byte for byte has
+// its code word read from LDS instead of HBM. Its descriptor in the
+// template copy of the slice table (CsrDev::sl_t) carries t + 1 in the high
+// half of its width (widths are at most 64).
+constexpr int kVT = 8388608;
+constexpr int kVtMax = 8;
+constexpr int kVtWidthMask = 0xffff;
 
 struct SellSlice {
   int64_t voff;  // first value of the slice (entries)
@@ -139,7 +149,22 @@ struct CsrDev {
   // SELL-P pattern is {-D, (-a,) -1, 0, 1, (a,) D} with D = 128 march_k rows
   // at pool base march_pat; march_len: planes per run (0: fill the grid)
   int march_k = 0, march_a = 0, march_pat = -1, march_len = 0;
+  // value-code templates (kVT): the slice table with template ids, the
+  // templates (nvt x 64 words of 4-bit codes)
+  const SellSlice *sl_t = nullptr;
+  const void *vct = nullptr;
+  int nvt = 0;
 };
+
+// The templates apply to the pipelined 4-bit value-code walks (bits 524288,
+// 262144; the consecutive walk and the plane march) of a matrix that has
+// them, when the requested variant asks for them: spmv_variant keeps kVT and
+// the kernel arguments take the template slice table under exactly this
+// condition.
+__host__ __device__ inline bool vt_active(const CsrDev &A) {
+  return (A.variant & kVT) && A.sl_t && A.vct && A.nvt > 0 && A.svc4 && A.svc && A.sl &&
+         A.sell_kind && A.sell_maxw <= 8 && (A.variant & 524288) && (A.variant & 262144);
+}
 
 template <typename T> struct Launch {
   static int grid_rows(int nrb);
@@ -236,6 +261,13 @@ template <typename T> struct Launch {
 
 // axpby modes
 enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
+
+// value-code templates (cgx_abi.cpp build_value_templates): per slice the
+// hash of its 4-bit code chunk (0: wider than one chunk); the template slice
+// table of nt templates, exact byte matches only (*count: matched slices)
+hipError_t vc_hash(const CsrDev &A, unsigned long long *hash, hipStream_t s);
+hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, SellSlice *sl_t,
+                    unsigned *count, hipStream_t s);
 
 // the SpMV variant a launch on A uses (dtype: CGX_F64 / CGX_F32)
 int launch_variant(const CsrDev &A, int dtype);

@@ -303,6 +303,9 @@ struct CsrArgs {
   // of k_spmv_dot_push): the SpMV's work split and partials use blockIdx -
   // wg0 of gridDim - wg0 workgroups (a multiple of 8 keeps the XCD groups)
   int wg0;
+  // value-code templates (kVT; sl is then the template slice table)
+  const unsigned long long *vct;
+  int nvt;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -787,6 +790,7 @@ __device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__rest
 // ---------------------------------------------------------------------------
 template <typename T> struct SellLds {
   T vdict[kVcDict];  // value-code dictionary (variant bit 32768)
+  unsigned long long vt[kVtMax * 64];  // value-code templates (variant bit kVT)
   T red[4 * kMaxRed];
   int flag;
   int rp[1];  // unused (keeps the SpmvLds member set)
@@ -1096,7 +1100,8 @@ __device__ __forceinline__ void spmv_sellp(const CsrArgs &A, const Gather &x, Ep
 // sums are the SELL-P sums, bit for bit.
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x, Epi &epi,
-                                              const T *__restrict__ vd, int s) {
+                                              const T *__restrict__ vd, int s,
+                                              const unsigned long long *vt = nullptr) {
   constexpr bool NT = (V & 2) != 0;
   const Ull2 *__restrict__ codes = static_cast<const Ull2 *>(A.svc);
   const auto *cs = (const __attribute__((address_space(4))) SellSlice *)A.sl;
@@ -1104,7 +1109,10 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
   const int lane = threadIdx.x & 63;
   const int si = __builtin_amdgcn_readfirstlane(s);
   const int64_t coff = cs[si].ioff;
-  const int pbase = cs[si].dict, W = cs[si].width;
+  // kVT: the template slice table's width carries the template id + 1 in
+  // its high half (0: the slice streams its own chunk)
+  const int wraw = cs[si].width, pbase = cs[si].dict, W = wraw & kVtWidthMask;
+  const int tid = (wraw >> 16) - 1;
   const int r0 = si * (2 * kSellRows) + 2 * lane;
   const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
   const int rc0 = l0 ? r0 : (int)A.n - 1, rc1 = l1 ? r0 + 1 : (int)A.n - 1;
@@ -1120,7 +1128,12 @@ __device__ __forceinline__ void sellpv_slice2(const CsrArgs &A, const Gather &x,
   for (int c = 0; c < W; c += 8) {
     Ull2 cw;
     if constexpr (C4) {
-      cw.x = ldg<NT>(codes4 + coff + (int64_t)(c >> 3) * kSellRows + lane);
+      if constexpr ((V & kVT) != 0) {  // template slice (one chunk): from LDS
+        cw.x = tid >= 0 ? vt[tid * 64 + lane]
+                        : ldg<NT>(codes4 + coff + (int64_t)(c >> 3) * kSellRows + lane);
+      } else {
+        cw.x = ldg<NT>(codes4 + coff + (int64_t)(c >> 3) * kSellRows + lane);
+      }
       cw.y = 0;
     } else {
       cw = ldg<NT>(codes + coff + (int64_t)(c >> 3) * kSellRows + lane);
@@ -1206,7 +1219,8 @@ template <> __device__ __forceinline__ float wave_shl1(float v, float edge) {
 // own gathers. Same sums in the same order as sellpv_slice2.
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather &x, Epi &epi,
-                                                 const T *__restrict__ vd) {
+                                                 const T *__restrict__ vd,
+                                                 const unsigned long long *vt) {
   constexpr bool NT = (V & 2) != 0;
   constexpr bool C4 = (V & 262144) != 0;
   constexpr bool CR = (V & 1048576) != 0;  // stencil slices: +-1 by lane shifts
@@ -1220,8 +1234,17 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
   int s, step, end, lo;
   sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   if (s >= end) return;
-  auto code_at = [&](int64_t coff) {
+  // tid: the slice's template (kVT; -1: it streams its own chunk)
+  auto code_at = [&](int64_t coff, int tid) {
     Ull2 cw;
+    if constexpr ((V & kVT) != 0) {
+      // template slice (uniform): the chunk comes from LDS, no HBM read
+      if (tid >= 0) {
+        cw.x = vt[tid * 64 + lane];
+        cw.y = 0;
+        return cw;
+      }
+    }
     if constexpr (C4) {
       cw.x = ldg<NT>(codes4 + coff + lane);
       cw.y = 0;
@@ -1231,14 +1254,14 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     return cw;
   };
   int si = __builtin_amdgcn_readfirstlane(slice_at(A, A.rev ? lo + end - 1 - s : s));
-  int W = cs[si].width;
+  int W = cs[si].width & kVtWidthMask;
   int o[8];
   {
     const int pb = cs[si].dict;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = pat[pb + min(j, W - 1)];
   }
-  Ull2 cwA = code_at(cs[si].ioff), cwB;
+  Ull2 cwA = code_at(cs[si].ioff, (cs[si].width >> 16) - 1), cwB;
   // slice si is interior when the pairs of its lowest and highest offset
   // (o[0], o[7] = o[W-1]: the pattern is sorted) lie inside x for every
   // lane, dead lanes of a last partial slice included, and byte offsets
@@ -1257,7 +1280,8 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     const bool has_next = ns < end;
     const int nk = has_next ? ns : s;
     const int sn = __builtin_amdgcn_readfirstlane(slice_at(A, A.rev ? lo + end - 1 - nk : nk));
-    const int Wn = cs[sn].width, pbn = cs[sn].dict;
+    const int wrn = cs[sn].width, pbn = cs[sn].dict;
+    const int Wn = wrn & kVtWidthMask;
     const int64_t coffn = cs[sn].ioff;
     const int r0 = si * (2 * kSellRows) + 2 * lane;
     const bool l0 = r0 < A.n, l1 = r0 + 1 < A.n;
@@ -1337,7 +1361,7 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
     int on[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) on[j] = pat[pbn + min(j, Wn - 1)];
-    cwn = code_at(coffn);
+    cwn = code_at(coffn, (wrn >> 16) - 1);
     __builtin_amdgcn_sched_barrier(0);
     T acc0 = T(0), acc1 = T(0);
 #pragma unroll
@@ -1398,7 +1422,8 @@ __device__ __forceinline__ void spmv_sellpv_pipe(const CsrArgs &A, const Gather 
 // (one code chunk per slice: slice s's codes at chunk s).
 template <typename T, int V, bool S3, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather &x, Epi &epi,
-                                                  const T *__restrict__ vd) {
+                                                  const T *__restrict__ vd,
+                                                  const unsigned long long *vt) {
   constexpr bool NT = (V & 2) != 0;
   constexpr bool C4 = (V & 262144) != 0;
   constexpr int H = 2 * kSellRows;
@@ -1423,8 +1448,16 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
   const bool off32 = (uint64_t)A.nx * sizeof(T) < (uint64_t(1) << 32);
   int it, step, end, lo;
   sell_range(K * Z, A.wg0, it, step, end, lo);
-  auto code_at = [&](int sl) {
+  // tid: the slice's template (kVT; -1: it streams its own chunk)
+  auto code_at = [&](int sl, int tid) {
     Ull2 cw;
+    if constexpr ((V & kVT) != 0) {
+      if (tid >= 0) {
+        cw.x = vt[tid * 64 + lane];
+        cw.y = 0;
+        return cw;
+      }
+    }
     if constexpr (C4) {
       cw.x = ldg<NT>(codes4 + (int64_t)sl * kSellRows + lane);
       cw.y = 0;
@@ -1442,12 +1475,18 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
   asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
   const Int2 *__restrict__ cdw = reinterpret_cast<const Int2 *>(
       reinterpret_cast<const char *>(A.sl) + offsetof(SellSlice, dict));
+  using Desc = Int2;
   auto desc = [&](int sl) { return cdw[(int64_t)sl * (sizeof(SellSlice) / sizeof(Int2)) + zv]; };
+  // the slice's template (kVT: the width's high half; -1: none)
+  auto dio = [&](const Desc &d) {
+    if constexpr ((V & kVT) != 0) return (__builtin_amdgcn_readfirstlane(d.y) >> 16) - 1;
+    else return -1;
+  };
   auto uni = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
   // slice sl walks the march pattern: its descriptor names the pattern, its
   // +-D neighbours exist (whole slices of rows), every pair lies inside x
   auto fast = [&](int sl, int dict, int w) {
-    return off32 && dict == A.mpat && w == W7 && sl >= K && sl + K < nfull;
+    return off32 && dict == A.mpat && (w & kVtWidthMask) == W7 && sl >= K && sl + K < nfull;
   };
   for (; it < end; it += step) {
     const int z = it / K, c = it - z * K;
@@ -1461,8 +1500,8 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
       PV gm, gp;
       T edge;
     };
-    auto issue = [&](int sl, bool fs, Batch &b) {
-      b.cw = code_at(sl);
+    auto issue = [&](int sl, bool fs, int io, Batch &b) {
+      b.cw = code_at(sl, io);
       const int fr = sl * H;
       const unsigned rb = (unsigned)min(fr + 2 * lane, nxm2) * (unsigned)sizeof(T);
       if constexpr (S3 && (V & 16) != 0) {
@@ -1524,7 +1563,7 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
         }
         epi.row2(r0, acc0, acc1, true, true);
       } else {
-        sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd, s);
+        sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd, s, vt);
         // drain: this path's load count is not fixed (a loop over code
         // chunks); a merge with an unknown count would make the compiler
         // wait vmcnt(0) before the next descriptor on every step
@@ -1537,7 +1576,7 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
     // argument, never by copy: a copy of a register whose load is in flight
     // waits for it (the loop below is unrolled four times so every role
     // returns to its register).
-    auto stepf = [&](int &s, bool &f, const Int2 &dcur, Int2 &dnew, const Batch &bc, Batch &bn,
+    auto stepf = [&](int &s, bool &f, const Desc &dcur, Desc &dnew, const Batch &bc, Batch &bn,
                      const PV &cm, const PV &c0, const PV &cp, PV &cnn) {
       const int sn = s + K;
       const bool has_next = sn <= last;
@@ -1546,7 +1585,7 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
       const int snk = has_next ? sn : s;
       const int snn = min(snk + K, nsl - 1);
       dnew = desc(snn);
-      issue(snk, fn, bn);
+      issue(snk, fn, dio(dcur), bn);
       cnn = center(snn);
       __builtin_amdgcn_sched_barrier(0);
       sum(s, f, bc, cm, c0, cp);
@@ -1558,12 +1597,12 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
     // descriptor of s + K
     // descriptor of s + K (the first step's) early: the first step waits
     // for it, and so for every load issued before it
-    const Int2 d0 = desc(s);
-    Int2 dA = desc(min(s + K, nsl - 1)), dB;
+    const Desc d0 = desc(s);
+    Desc dA = desc(min(s + K, nsl - 1)), dB;
     PV c0 = center(max(s - K, 0)), c1 = center(s), c2, c3;
     bool f = fast(s, uni(d0.x), uni(d0.y));
     Batch bA, bB;
-    issue(s, f, bA);
+    issue(s, f, dio(d0), bA);
     c2 = center(min(s + K, nsl - 1));
     for (;;) {
       if (!stepf(s, f, dA, dB, bA, bB, c0, c1, c2, c3)) break;
@@ -1576,26 +1615,28 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
 
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, Epi &epi,
-                                            T *vd) {
+                                            T *vd, unsigned long long *vt) {
   const T *__restrict__ src = static_cast<const T *>(A.svdict);
   for (int i = threadIdx.x; i < kVcDict; i += kBlock) vd[i] = src[i];
+  if constexpr ((V & kVT) != 0)  // the value-code templates next to the dictionary
+    for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) vt[i] = A.vct[i];
   __syncthreads();
   if constexpr ((V & 2097152) != 0) {
     if (A.mk > 0) {
-      if (A.mo > 0) spmv_sellpv_march<T, V, true, Epi, Gather>(A, x, epi, vd);
-      else spmv_sellpv_march<T, V, false, Epi, Gather>(A, x, epi, vd);
+      if (A.mo > 0) spmv_sellpv_march<T, V, true, Epi, Gather>(A, x, epi, vd, vt);
+      else spmv_sellpv_march<T, V, false, Epi, Gather>(A, x, epi, vd, vt);
       return;
     }
   }
   if constexpr ((V & 524288) != 0) {
-    spmv_sellpv_pipe<T, V, Epi, Gather>(A, x, epi, vd);
+    spmv_sellpv_pipe<T, V, Epi, Gather>(A, x, epi, vd, vt);
     return;
   }
   int s, step, end, lo;
   sell_range((int)A.nsl, A.wg0, s, step, end, lo);
   for (; s < end; s += step)
     sellpv_slice2<T, V, Epi, Gather>(A, x, epi, vd,
-                                     slice_at(A, A.rev ? lo + end - 1 - s : s));
+                                     slice_at(A, A.rev ? lo + end - 1 - s : s), vt);
 }
 
 // LDS layout of a variant's kernel
@@ -1608,7 +1649,7 @@ using LdsOf = typename std::conditional<
 template <typename T, int V, class Epi, class Gather>
 __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__ val,
                                          const Gather &x, Epi &epi, LdsOf<T, V> &sm) {
-  if constexpr ((V & 32768) != 0) spmv_sellpv<T, V, Epi, Gather>(A, x, epi, sm.vdict);
+  if constexpr ((V & 32768) != 0) spmv_sellpv<T, V, Epi, Gather>(A, x, epi, sm.vdict, sm.vt);
   else if constexpr ((V & 8192) != 0) spmv_sellp<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 4096) != 0) spmv_sell2<T, V, Epi, Gather>(A, x, epi);
   else if constexpr ((V & 2048) != 0 && (V & 8) != 0) spmv_sell_pipe<T, V, Epi, Gather>(A, x, epi);
@@ -1846,7 +1887,17 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
 // value-code SELL-P form needs 8 (its persistent grid of kMaxGrid workgroups
 // is then resident at once); the rest take what they get.
 template <int V> struct SpmvWaves {
-  static constexpr int w = (V & 32768) && (V & (65536 | 131072)) ? 8 : 1;
+  // the plane march with templates: held to the 4 waves per SIMD (128
+  // VGPRs, a 12-byte spill) the streamed-code march gets (it took 130 and 3)
+  static constexpr int w = (V & 32768) && (V & (65536 | 131072)) ? 8
+                           : ((V & kVT) && (V & 2097152)) ? 4
+                                                          : 1;
+};
+// k_spmv_fd: the same except the template march (held to 4 waves it
+// spilled 140 bytes; it takes 152 VGPRs, 3 waves, against 169 and 2 for the
+// streamed-code march)
+template <int V> struct FdWaves {
+  static constexpr int w = ((V & kVT) && (V & 2097152)) ? 1 : SpmvWaves<V>::w;
 };
 
 template <typename T, int V>
@@ -1898,7 +1949,7 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
 // where the host reads the final r.r — and, in slot 0, opens a new group of
 // deferred x updates (ran[] cleared; the slot-3 flush has applied the last).
 template <typename T, int V>
-__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd(
+__global__ __launch_bounds__(kBlock, FdWaves<V>::w) void k_spmv_fd(
     CsrArgs A, const T *__restrict__ val, const T *__restrict__ r, const T *__restrict__ pold,
     T *__restrict__ pc, T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
     int np_rr) {
@@ -2488,6 +2539,62 @@ __global__ __launch_bounds__(kBlock) void k_vc_narrow(const unsigned char *__res
   }
 }
 
+// ---- value-code templates (kVT, cgx_abi.cpp build_value_templates) --------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long wave_xor64(unsigned long long h) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)h, o, 64);
+    const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(h >> 32), o, 64);
+    h ^= ((unsigned long long)hi << 32) | lo;
+  }
+  return h;
+}
+// one wave per slice: a hash of its 64-word 4-bit code chunk (0: the slice
+// is wider than one chunk, no template)
+__global__ __launch_bounds__(kBlock) void k_vc_hash(const SellSlice *__restrict__ sl, int64_t nsl,
+                                                    const unsigned long long *__restrict__ c4,
+                                                    unsigned long long *__restrict__ hash) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (s >= nsl) return;  // wave-uniform
+  const SellSlice m = sl[s];
+  unsigned long long h = 0;
+  if (m.width <= 8) h = mix64(c4[m.ioff + lane] ^ (0x9E3779B97F4A7C15ull * (unsigned)(lane + 1)));
+  h = wave_xor64(h);
+  if (lane == 0) hash[s] = m.width <= 8 ? (h ? h : 1) : 0;
+}
+// one wave per slice: the template slice table — slice s's descriptor with
+// (t + 1) << 16 added to its width when its chunk equals template t in
+// every byte (checked here, whatever the hashes said), else unchanged;
+// *count: matched slices
+__global__ __launch_bounds__(kBlock) void k_vc_match(const SellSlice *__restrict__ sl, int64_t nsl,
+                                                     const unsigned long long *__restrict__ c4,
+                                                     const unsigned long long *__restrict__ tmpl,
+                                                     int nt, SellSlice *__restrict__ sl_t,
+                                                     unsigned *count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (s >= nsl) return;  // wave-uniform
+  SellSlice m = sl[s];
+  int hit = -1;
+  if (m.width <= 8) {
+    const unsigned long long w = c4[m.ioff + lane];
+    for (int t = 0; t < nt && hit < 0; ++t)
+      if (__all(w == tmpl[t * 64 + lane])) hit = t;
+  }
+  if (lane == 0) {
+    if (hit >= 0) {
+      m.width |= (hit + 1) << 16;
+      atomicAdd(count, 1u);
+    }
+    sl_t[s] = m;
+  }
+}
+
 // Poisson rows [row_begin, row_end): columns ascending (-z,-y,-x,d,+x,+y,+z).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_poisson(int dim, int nx, int ny, int nz,
@@ -2527,10 +2634,16 @@ inline int elem_grid(int64_t n, int per_thread) {
 }
 
 inline CsrArgs args(const CsrDev &A) {
-  return CsrArgs{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
-                 A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
-                 A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4,
-                 A.march_k, A.march_a, A.march_pat, A.march_len};
+  CsrArgs a{A.rowptr, A.col,   A.rb,   A.rbk,  A.nrb,  A.n,
+            A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
+            A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4,
+            A.march_k, A.march_a, A.march_pat, A.march_len};
+  if (vt_active(A)) {  // the same condition spmv_variant keeps kVT under
+    a.sl = A.sl_t;
+    a.vct = static_cast<const unsigned long long *>(A.vct);
+    a.nvt = A.nvt;
+  }
+  return a;
 }
 
 }  // namespace
@@ -2875,7 +2988,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
       return 32768 | 8192 |
              (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
                    (A.sell_maxw <= 8 ? 524288 | 1048576 : 0) |
-                   (A.sell_maxw <= 8 && A.march_k > 0 ? 2097152 : 0)));
+                   (A.sell_maxw <= 8 && A.march_k > 0 ? 2097152 : 0))) |
+             (vt_active(A) ? kVT : 0);
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -2908,8 +3022,9 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 // non-temporal, 4 paired loads), 12-15 (+8 pipelined), 264-267 (quads);
 // dictionary SELL 2048/2050/2056/2058/6144/6146; SELL-P 8192/8194 (+16384:
 // 24576/24578); value-code SELL-P and its pipelined / stencil / plane-march
-// loops. (Round 1's half-tile, three-stage and wave-tile CSR forms, negative
-// results recorded in DESIGN.md §8, were retired in round 3.) One-off
+// loops. (Round 1's half-tile, three-stage and wave-tile CSR forms and
+// round 3's row-gather form, negative results recorded in DESIGN.md §8, are
+// not built.) One-off
 // kernels (cg init, accuracy) run CSR-stream: every form gives the same
 // per-row sums.
 #define CGX_SPMV_SWITCH(v, KERNEL, ...)                        \
@@ -2956,6 +3071,12 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 3710978: CGX_LAUNCH_V(KERNEL, 3710978, __VA_ARGS__);  \
     case 3973120: CGX_LAUNCH_V(KERNEL, 3973120, __VA_ARGS__);  \
     case 3973122: CGX_LAUNCH_V(KERNEL, 3973122, __VA_ARGS__);  \
+    case 9216000: CGX_LAUNCH_V(KERNEL, 9216000, __VA_ARGS__);  \
+    case 9216002: CGX_LAUNCH_V(KERNEL, 9216002, __VA_ARGS__);  \
+    case 10264576: CGX_LAUNCH_V(KERNEL, 10264576, __VA_ARGS__);\
+    case 10264578: CGX_LAUNCH_V(KERNEL, 10264578, __VA_ARGS__);\
+    case 12361728: CGX_LAUNCH_V(KERNEL, 12361728, __VA_ARGS__);\
+    case 12361730: CGX_LAUNCH_V(KERNEL, 12361730, __VA_ARGS__);\
     default: return hipErrorInvalidValue;                      \
   }
 
@@ -2970,7 +3091,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(267) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578)  \
   X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
   X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122) X(40978)     \
-  X(106498) X(172034) X(303122) X(827410)
+  X(106498) X(172034) X(303122) X(827410) X(9216000) X(9216002) X(10264576) X(10264578)     \
+  X(12361728) X(12361730)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \
@@ -3120,7 +3242,8 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
 #define CGX_FD_LIST(X)                                                                 \
   X(13) X(15) X(8192) X(8194) X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) \
   X(827392) X(827394) X(1613824) X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) \
-  X(3973120) X(3973122)
+  X(3973120) X(3973122) X(9216000) X(9216002) X(10264576) X(10264578) X(12361728)      \
+  X(12361730)
 
 // mode 2 (k_spmv_fused): mode 4's forms, plain CSR-stream and the
 // dictionary SELL forms small matrices take
@@ -3195,7 +3318,7 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
 #define CGX_PUSH_LIST(X)                                                                \
   X(2048) X(2050) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578) X(40960) X(40962)  \
   X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824) X(1613826)     \
-  X(1875968) X(1875970)
+  X(1875968) X(1875970) X(9216000) X(9216002) X(10264576) X(10264578)
 
 template <typename T> static const void *spmv_push_kernel(int v) {
   switch (v) {
@@ -3410,6 +3533,20 @@ hipError_t Launch<T>::vc_narrow(const void *codes8, void *codes4, int64_t chunks
                                 hipStream_t s) {
   hipLaunchKernelGGL(k_vc_narrow, dim3(elem_grid(chunks, 4)), dim3(kBlock), 0, s,
                      (const unsigned char *)codes8, (unsigned char *)codes4, chunks);
+  return hipGetLastError();
+}
+
+hipError_t vc_hash(const CsrDev &A, unsigned long long *hash, hipStream_t s) {
+  const int g = (int)((A.nsl + 3) / 4);
+  hipLaunchKernelGGL(k_vc_hash, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
+                     (const unsigned long long *)A.svc4, hash);
+  return hipGetLastError();
+}
+hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, SellSlice *sl_t,
+                    unsigned *count, hipStream_t s) {
+  const int g = (int)((A.nsl + 3) / 4);
+  hipLaunchKernelGGL(k_vc_match, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
+                     (const unsigned long long *)A.svc4, tmpl, nt, sl_t, count);
   return hipGetLastError();
 }
 

@@ -158,6 +158,8 @@ struct cgx_csr {
   void *d_sell_mask = nullptr;  // SELL-P slot masks
   void *d_sell_vc = nullptr, *d_sell_vdict = nullptr;  // SELL-P value codes, dictionary
   void *d_sell_vc4 = nullptr;                          // 4-bit value codes
+  void *d_sell_sl_t = nullptr, *d_vct = nullptr;       // value-code templates (kVT)
+  int64_t vt_slices = 0;                               // slices that read a template
   // partitioned SELL matrix: slices without ghost columns, then those with
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;

@@ -102,6 +102,10 @@ int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
  * cgx_csr_create when the SELL-P copy exists and the matrix has that few
  * distinct values; $CGX_VALUE_CODES=0 disables it), 0 when it has none. */
 int cgx_csr_value_codes(cgx_csr *csr, int *n_values);
+/* Value-code templates (variant bit 8388608): the number of distinct 4-bit
+ * code chunks stored once and read from LDS, and the slices that use one
+ * (0 / 0: none). */
+int cgx_csr_templates(cgx_csr *csr, int *n_templates, int64_t *slices);
 /* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
  * *stride = slices (of 128 rows) between a slice and its +-D neighbour
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D

@@ -194,3 +194,87 @@ def test_cg_every_value_code_form_in_the_loop(oracle, monkeypatch, dim, n):
     for v in VC + VC4:
         np.testing.assert_array_equal(out[v][0], out[8194][0], err_msg=f"variant {v}")
         assert out[v][1] == out[8194][1], v
+
+
+# value-code templates (variant bit 8388608): the pipelined 4-bit forms
+# (plain, stencil and plane march; default / non-temporal loads) with the
+# slices whose code chunk equals a stored template reading it from LDS
+VT = [9209856, 9209858, 10258432, 10258434, 12355584, 12355586]
+
+
+def templates(m):
+    nt, sl = C.c_int(), C.c_int64()
+    check(lib().cgx_csr_templates(m.schedule(), C.byref(nt), C.byref(sl)))
+    return nt.value, sl.value
+
+
+def stream_bytes(m):
+    b = C.c_int64()
+    check(lib().cgx_csr_stream_bytes(m.schedule(), C.byref(b)))
+    return b.value
+
+
+@pytest.mark.parametrize("case", ["p3d_64", "p2d_512x256", "p3d_128x96x40"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_value_code_templates_bitexact(queue, oracle, case, dtype):
+    """A slice reads its code chunk from a template only when the two are
+    equal byte for byte (checked on the device at build), so Ap is
+    bit-identical to the streamed-code forms and to the oracle; the stream
+    shrinks by the template slices' chunks."""
+    rp, cl, vl = {"p3d_64": lambda: oracle.poisson(3, 64, 64, 64),
+                  "p2d_512x256": lambda: oracle.poisson(2, 512, 256, 1),
+                  "p3d_128x96x40": lambda: oracle.poisson(3, 128, 96, 40)}[case]()
+    n = len(rp) - 1
+    A = Matrix(queue, vl, cl, rp, dtype=dtype)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    nt, nsl_t = templates(A)
+    nsl = (n + 127) // 128
+    assert 1 <= nt <= 8 and 64 <= nsl_t <= nsl, (nt, nsl_t, nsl)
+    x = np.random.default_rng(11).standard_normal(n)
+    x[[3, n // 2]] = [np.inf, -0.0]
+    base = [821250, 1869826]
+    out = spmv_all(queue, A, x, base + VT, dtype)
+    ref = oracle.spmv(rp, cl, vl, x) if dtype == np.float64 else out[821250]
+    for k in base + VT:
+        np.testing.assert_array_equal(out[k], ref, err_msg=f"variant {k}")
+    check(lib().cgx_csr_set_variant(A.schedule(), 1869826))
+    b0 = stream_bytes(A)
+    check(lib().cgx_csr_set_variant(A.schedule(), 10258434))
+    v = C.c_int()
+    check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
+    assert v.value == 10264578
+    assert stream_bytes(A) == b0 - 512 * nsl_t + 512 * nt
+
+
+def test_value_code_templates_refused_without_them(queue, oracle, monkeypatch):
+    monkeypatch.setenv("CGX_VT", "0")
+    rp, cl, vl = oracle.poisson(3, 32, 32, 32)
+    A = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(A.schedule(), 3))
+    assert templates(A) == (0, 0)
+    with pytest.raises(CgxError, match="templates"):
+        check(lib().cgx_csr_set_variant(A.schedule(), VT[0]))
+
+
+@pytest.mark.parametrize("mode", [1, 3, 4])
+def test_value_code_templates_in_the_solver(oracle, monkeypatch, mode):
+    """CG with the template form equals CG with streamed codes bit for bit
+    (modes 1, 3 and 4), and the oracle to the §8(c) tolerances."""
+    # x lines of 64 rows: a slice is two of them, so the interior slices of
+    # every plane share one chunk (a template)
+    rp, cl, vl = oracle.poisson(3, 64, 64, 48)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    xs = {}
+    for v in (1869826, 10258434):
+        monkeypatch.setenv("CGX_SPMV_VARIANT", str(v))
+        cg = cga.CG.createCG()
+        cg.mode = mode
+        cg.setMatrix(vl, cl, rp)
+        cg.setTarget(b)
+        cg.solve(1e-3)  # ||b|| = 4e7: 2e-11 relative (1e-8 sits at fp64's floor)
+        xs[v] = (cg.extract(), cg.iterations)
+    np.testing.assert_array_equal(xs[10258434][0], xs[1869826][0])
+    assert xs[10258434][1] == xs[1869826][1]
+    xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-3)
+    assert abs(xs[1869826][1] - res.iterations) <= 2
+    assert rel(xs[10258434][0], xr) <= 1e-10
