@@ -26,3 +26,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -k 10 600 python tools/configs_bench.py > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; tail -20 $OUT/configs.log; exit 1; }
 cut -c1-240 $OUT/configs.log
+timeout -k 10 400 bash tools/gpu_slab.sh $TAG/slab > $OUT/slab_all.log 2>&1 || { echo SLAB_FAIL; tail -20 $OUT/slab_all.log; exit 1; }
+cat $OUT/slab_all.log
