@@ -269,19 +269,41 @@ def run(args) -> None:
     strong = not args.weak
     # ---- communicator (N > 1) ----------------------------------------------
     transport = "single"
+    rccl_note = None
     if world > 1 and args.transport in ("host", "host-peer"):
         from conjugategradient_amd.hostcomm import HostTransport
         ht = HostTransport()
         ht.attach(q)
         transport = "host"
     elif world > 1:
+        # RCCL; with --transport auto, a node where it does not come up
+        # (every rank's outcome, agreed over gloo) keeps the host transport
+        # for setup and tries the device peer transport for the iteration
         uid = C.create_string_buffer(128)
+        rc = 0
         if rank == 0:
-            check(L.cgx_nccl_unique_id(uid, 128))
-        obj = [bytes(uid.raw) if rank == 0 else None]
+            rc = L.cgx_nccl_unique_id(uid, 128)
+        obj = [(bytes(uid.raw), rc) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        check(L.cgx_dist_init(q.handle, rank, world, obj[0], 128))
-        transport = "rccl"
+        if obj[0][1] == 0:
+            rc = L.cgx_dist_init(q.handle, rank, world, obj[0][0], 128)
+        else:
+            rc = obj[0][1]
+        why = L.cgx_last_error().decode() if rc else ""
+        ok = torch.tensor([0.0 if rc == 0 else 1.0], dtype=torch.float64)
+        dist.all_reduce(ok)
+        if ok.item() == 0.0:
+            transport = "rccl"
+        elif args.transport == "auto":
+            if rc == 0:  # this rank's communicator came up alone: a fresh context
+                q = cga.Queue(dev)
+            from conjugategradient_amd.hostcomm import HostTransport
+            ht = HostTransport()
+            ht.attach(q)
+            transport = "host"
+            rccl_note = f"RCCL unavailable ({why or 'on another rank'}): host setup transport"
+        else:
+            raise SystemExit(f"bench.py: RCCL init failed: {why or 'on another rank'}")
     wr, ww = C.c_int(0), C.c_int(0)
     check(L.cgx_dist_rank(q.handle, C.byref(wr), C.byref(ww)))
     if ww.value != args.gpus or ww.value != world:
@@ -478,6 +500,7 @@ def run(args) -> None:
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
                        "peer_fallback_reason": peer_note,
+                       "rccl_note": rccl_note,
                        "transport_validation": validation,
                        "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies",

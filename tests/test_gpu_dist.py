@@ -112,3 +112,20 @@ def test_bench_two_ranks_validates_peer_transport():
     assert v["ok"], v
     assert v["x_rel_peer_vs_setup"] <= 1e-10
     assert line["config"]["transport"].startswith("peer")
+
+
+def test_bench_two_ranks_auto_transport_on_one_gpu():
+    """--transport auto (the driver's N > 1 default) where RCCL does not come
+    up: on this one-GPU box RCCL refuses two ranks on one device, so every
+    rank keeps the host transport for setup, validates the device peer
+    transport against it and times the run over the peer transport."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--grid", "64",
+           "--steps", "20", "--warmup", "5", "--no-cpu", "--profile-steps", "0",
+           "--master-port", str(_port())]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = line["config"]
+    assert cfg["rccl_note"] and "host setup transport" in cfg["rccl_note"], cfg
+    assert cfg["transport_validation"]["ok"], cfg["transport_validation"]
+    assert cfg["transport"] == "peer (setup: host)"
