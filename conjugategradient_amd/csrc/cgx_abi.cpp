@@ -134,7 +134,7 @@ template <class F> int timed(cgx_cg *cg, int kid, hipStream_t s, F &&launch) {
 // iterations after the stop return at entry and would skew the averages.
 int harvest_events(cgx_cg *cg, int64_t active_iters) {
   int64_t iter_seen = 0;
-  const int last_kid = (cg->fused || cg->fdefer) ? 2 : 3;
+  const int last_kid = cg->coop ? 1 : (cg->fused || cg->fdefer) ? 2 : 3;
   for (auto &pr : cg->ev_pending) {
     const int kid = pr.first;
     float ms = 0;
@@ -374,6 +374,28 @@ template <typename T> int enqueue_iter_fused(cgx_cg *cg, int slot) {
   return CGX_OK;
 }
 
+// bodies per mode-5 launch: 8 poll intervals (a launch ends early at the stop,
+// so a larger chunk costs nothing but the host's view of progress)
+int64_t coop_chunk(const cgx_cg *cg) { return (int64_t)cg->poll_every * 8; }
+
+// Mode 5: `bodies` bodies from `slot` in one persistent launch
+int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
+  const CsrDev &A = cg->A->dev;
+  const int m = (int)std::min<int64_t>(bodies, 1 << 30);
+  return timed(cg, 1, cg->ctx->stream, [&] {
+    return cg_coop(cg->n, cg->coop_r, A.rowptr, A.col, (const double *)A.val, (double *)cg->x,
+                   (double *)cg->r, (double *)cg->p, (double *)cg->p2,
+                   (CgScalars<double> *)cg->st, slot, m, (CoopWs *)cg->coop_ws, cg->coop_ticks,
+                   cg->ctx->stream);
+  });
+}
+
+// $CGX_COOP_R: mode 5's rows per thread (1, 2, 4; unset: the fewest that fit)
+int coop_want_r() {
+  const char *e = std::getenv("CGX_COOP_R");
+  return e ? std::atoi(e) : 0;
+}
+
 int enqueue_iter_any(cgx_cg *cg, int slot) {
   if (cg->fdefer)
     return cg->dtype == CGX_F32 ? enqueue_iter_fdefer<float>(cg, slot)
@@ -473,7 +495,7 @@ int build_graph(cgx_cg *cg, int slot0, int64_t iters, hipGraphExec_t *out) {
 bool graph_ok(const cgx_cg *cg) {
   // RCCL / host-transport calls are kept out of captured graphs (the peer
   // transport's iteration is all kernels); timing needs eager launches
-  return cg->use_graph && !cg->timing && (!cg->A->dist || cg->A->peer.on);
+  return cg->use_graph && !cg->timing && !cg->coop && (!cg->A->dist || cg->A->peer.on);
 }
 
 // The graph for a chunk of `iters` bodies from `slot0`: a cached one, else a
@@ -1923,9 +1945,18 @@ static bool fd_auto(const cgx_cg *cg) {
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
-  CGX_REQUIRE(mode >= 0 && mode <= 4, CGX_EINVAL,
+  CGX_REQUIRE(mode >= 0 && mode <= 5, CGX_EINVAL,
               "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
-              "4 fused with deferred x", mode);
+              "4 fused with deferred x, 5 persistent body", mode);
+  int coop_r = 0;
+  if (mode == 5) {
+    CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
+                "mode 5 (persistent body) runs f64 on a single device");
+    coop_r = coop_rows_per_thread(cg->n, coop_want_r());
+    CGX_REQUIRE(coop_r > 0, CGX_EUNSUPPORTED,
+                "mode 5 (persistent body) takes at most %lld rows (n = %lld)",
+                (long long)kCoopMaxG * kBlock * 4, (long long)cg->n);
+  }
   CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
               "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
   CGX_REQUIRE(mode != 2 || (cg->dtype == CGX_F32 ? Launch<float>::fused_supported(cg->A->dev)
@@ -1936,11 +1967,23 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
               CGX_EUNSUPPORTED, "mode 4 needs an f64 matrix in a production SpMV format "
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
   if (mode == 0) mode = fd_auto(cg) ? 4 : 3;
-  const bool f = mode == 2, d = mode == 3, fd = mode == 4;
-  if (f != cg->fused || d != cg->defer || fd != cg->fdefer) {
+  const bool f = mode == 2, d = mode == 3, fd = mode == 4, c = mode == 5;
+  if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop) {
     CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
     drop_graph(cg);
   }
+  if (c && !cg->coop_ws) {
+    DeviceGuard g(cg->ctx->device);
+    CGX_HIP(hipMalloc(&cg->coop_ws, sizeof(CoopWs)));
+    int clk_khz = 0;
+    if (hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, cg->ctx->device) !=
+            hipSuccess ||
+        clk_khz <= 0)
+      clk_khz = 100000;  // 100 MHz on gfx9
+    cg->coop_ticks = (long long)clk_khz * 1000 * 2;  // 2 s: a resident grid never waits so long
+  }
+  cg->coop = c;
+  if (c) cg->coop_r = coop_r;
   if ((d || fd) && !cg->pk[0]) {  // three more p buffers (with the ghost tail when partitioned)
     DeviceGuard g(cg->ctx->device);
     const size_t bytes = (size_t)(cg->n + cg->A->halo.n_ghost) * dtype_size(cg->dtype);
@@ -1977,7 +2020,7 @@ extern "C" int cgx_csr_fd_grid(cgx_csr *A, int *fd_grid, int *spmv_grid) {
 
 extern "C" int cgx_cg_get_mode(cgx_cg *cg, int *mode) {
   CGX_REQUIRE(cg && mode, CGX_EINVAL, "NULL argument");
-  *mode = cg->fdefer ? 4 : cg->defer ? 3 : cg->fused ? 2 : 1;
+  *mode = cg->coop ? 5 : cg->fdefer ? 4 : cg->defer ? 3 : cg->fused ? 2 : 1;
   return CGX_OK;
 }
 
@@ -1987,7 +2030,8 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   (void)hipStreamSynchronize(cg->ctx->stream);
   drop_graph(cg);
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
-  for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2]})
+  for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2],
+                  cg->coop_ws})
     if (p) (void)hipFree(p);
   cgx_csr *A = cg->A;
   cgx_ctx *ctx = cg->ctx;
@@ -2131,10 +2175,13 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   }
   while (!done && (remaining > 0 || !q.empty())) {
     if (remaining > 0 && q.size() < 2) {
-      const int64_t chunk = std::min<int64_t>(remaining, cg->poll_every);
+      // mode 5: one launch per chunk of coop_chunk bodies (it leaves at the stop)
+      const int64_t chunk = std::min<int64_t>(remaining, cg->coop ? coop_chunk(cg) : cg->poll_every);
       hipGraphExec_t ge = nullptr;
       if (use_graph && (rc = chunk_graph(cg, cg->slot, chunk, chunk == cg->poll_every, &ge))) break;
-      if (ge) {
+      if (cg->coop) {
+        if ((rc = enqueue_coop(cg, cg->slot, chunk))) break;
+      } else if (ge) {
         CGX_HIP(hipGraphLaunch(ge, s));
       } else {
         for (int64_t i = 0; i < chunk && rc == CGX_OK; ++i) rc = enqueue_iter_any(cg, (cg->slot + (int)i) & 3);

@@ -262,6 +262,27 @@ template <typename T> struct Launch {
 // axpby modes
 enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 
+// ---- persistent CG body (mode 5, cgx_coop.hip) -------------------------------
+constexpr int kCoopK = 8;       // entries per row held in registers
+constexpr int kCoopMaxG = 128;  // workgroups: at most one per CU on half the chip
+// exchange granules ({tag, half of a double}: two per workgroup and exchange),
+// zeroed before every launch
+struct CoopWs {
+  unsigned long long ga[2 * kCoopMaxG];  // p.Ap partials
+  unsigned long long gb[2 * kCoopMaxG];  // r.r partials
+  unsigned int tmo;                      // a workgroup's spin gave up
+  unsigned int pad[3];
+};
+// rows per thread (1, 2 or 4; `want` > 0 asks for one) for which n rows fit
+// kCoopMaxG workgroups; 0: none
+int coop_rows_per_thread(int64_t n, int want);
+// up to m bodies from slot0 in one launch (f64, single device): x, r, p0 in
+// and out in the standard layout, p1 scratch (n entries); stops as the
+// three-kernel body does, or sets st->stopped = 4 when a spin gave up
+hipError_t cg_coop(int64_t n, int R, const int *rowptr, const int *col, const double *val,
+                   double *x, double *r, double *p0, double *p1, CgScalars<double> *st, int slot0,
+                   int m, CoopWs *cw, long long ticks, hipStream_t s);
+
 // value-code templates (cgx_abi.cpp build_value_templates): per slice the
 // hash of its 4-bit code chunk (0: wider than one chunk); the template slice
 // table of nt templates, exact byte matches only (*count: matched slices)

@@ -181,6 +181,10 @@ struct cgx_cg {
   bool fused = false;   // two kernels per iteration (x/p update folded into SpMV)
   bool defer = false;   // mode 3: x updated once per 4 bodies from 4 p buffers
   bool fdefer = false;  // mode 4: p update folded into the SpMV, x deferred as mode 3
+  bool coop = false;    // mode 5: persistent body, one launch per chunk (cgx_coop.hip)
+  int coop_r = 0;       // its rows per thread
+  void *coop_ws = nullptr;  // cgx::CoopWs
+  long long coop_ticks = 0; // wall-clock ticks before an exchange spin gives up
   bool altdir = false;  // alternate the kernels' sweep directions (Infinity-Cache reuse)
   void *pk[3] = {nullptr, nullptr, nullptr};  // p buffers 1..3 of mode 3 (n + n_ghost)
   void *st = nullptr;   // cgx::CgScalars<T>

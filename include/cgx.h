@@ -186,11 +186,15 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * device, f64, production SpMV formats): two kernels per body, p_k = r +
  * beta p_{k-1} computed where the SpMV reads it and stored once into the
  * p ring, update_r with the stop rule, x from the four p buffers in slot 3
- * (72 N + matrix bytes per body against 78 N in mode 3).
+ * (72 N + matrix bytes per body against 78 N in mode 3); 5 persistent body
+ * (single device, f64, n <= 131072 rows): one launch runs a whole chunk of
+ * bodies, each with two grid-wide exchanges of the dot partials instead of
+ * three kernel boundaries; Ap bit-identical, the dots summed in another
+ * order (x equal to rounding). $CGX_COOP_R picks its rows per thread.
  * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
  * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
-/* the iteration structure in effect (1-4; auto resolved) */
+/* the iteration structure in effect (1-5; auto resolved) */
 int cgx_cg_get_mode(cgx_cg *cg, int *mode);
 /* mode 4's fused SpMV grid and the SpMV's: where they are equal mode 4 is
  * bit-identical to mode 1, else equal to rounding (one dot's sum order) */
