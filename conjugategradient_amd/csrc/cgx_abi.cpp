@@ -383,10 +383,11 @@ int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
   const CsrDev &A = cg->A->dev;
   const int m = (int)std::min<int64_t>(bodies, 1 << 30);
   return timed(cg, 1, cg->ctx->stream, [&] {
-    return cg_coop(cg->n, cg->coop_r, A.rowptr, A.col, (const double *)A.val, (double *)cg->x,
-                   (double *)cg->r, (double *)cg->p, (double *)cg->p2,
-                   (CgScalars<double> *)cg->st, slot, m, (CoopWs *)cg->coop_ws, cg->coop_ticks,
-                   cg->ctx->stream);
+    return cg_coop(cg->n, cg->coop_r, cg->coop_nt, cg->coop_tagr, A.rowptr, A.col, (const double *)A.val,
+                   (double *)cg->x, (double *)cg->r, (double *)cg->p, (double *)cg->p2,
+                   (unsigned long long *)cg->coop_rg, (CgScalars<double> *)cg->st, slot, m,
+                   (CoopWs *)cg->coop_ws, cg->coop_ticks,
+                   (unsigned long long *)cg->coop_trace, cg->coop_nap, cg->ctx->stream);
   });
 }
 
@@ -1952,7 +1953,9 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   if (mode == 5) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) runs f64 on a single device");
-    coop_r = coop_rows_per_thread(cg->n, coop_want_r());
+    if (const char *e = std::getenv("CGX_COOP_NT")) cg->coop_nt = std::atoi(e);
+    if (const char *e = std::getenv("CGX_COOP_NAP")) cg->coop_nap = std::max(0, std::atoi(e));
+    coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
     CGX_REQUIRE(coop_r > 0, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) takes at most %lld rows (n = %lld)",
                 (long long)kCoopMaxG * kBlock * 4, (long long)cg->n);
@@ -1975,6 +1978,12 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   if (c && !cg->coop_ws) {
     DeviceGuard g(cg->ctx->device);
     CGX_HIP(hipMalloc(&cg->coop_ws, sizeof(CoopWs)));
+    CGX_HIP(hipMalloc(&cg->coop_rg, (size_t)cg->n * 48));
+    if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
+    if (const char *e = std::getenv("CGX_COOP_TRACE"); e && std::atoi(e)) {
+      CGX_HIP(hipMalloc(&cg->coop_trace, kCoopTraceWords * sizeof(unsigned long long)));
+      CGX_HIP(hipMemset(cg->coop_trace, 0, kCoopTraceWords * sizeof(unsigned long long)));
+    }
     int clk_khz = 0;
     if (hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, cg->ctx->device) !=
             hipSuccess ||
@@ -2031,7 +2040,7 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   drop_graph(cg);
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
   for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2],
-                  cg->coop_ws})
+                  cg->coop_ws, cg->coop_rg, cg->coop_trace})
     if (p) (void)hipFree(p);
   cgx_csr *A = cg->A;
   cgx_ctx *ctx = cg->ctx;
@@ -2234,6 +2243,27 @@ extern "C" int cgx_cg_prepare(cgx_cg *cg, int64_t bodies) {
     slot = (int)((slot + chunk) & 3);
     remaining -= chunk;
   }
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *workgroups,
+                                 int *tagged) {
+  CGX_REQUIRE(cg && rows_per_thread && workgroups && tagged, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(cg->coop, CGX_ESTATE, "the solver is not in mode 5");
+  *rows_per_thread = cg->coop_r;
+  const int64_t per = (int64_t)cg->coop_nt * cg->coop_r;
+  *workgroups = (int)((cg->n + per - 1) / per);
+  *tagged = cg->coop_tagr ? 1 : 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_coop_trace(cgx_cg *cg, uint64_t *host, int64_t words) {
+  CGX_REQUIRE(cg && host, CGX_EINVAL, "NULL argument");
+  CGX_REQUIRE(cg->coop_trace, CGX_ESTATE, "no trace: set CGX_COOP_TRACE=1 before mode 5");
+  DeviceGuard g(cg->ctx->device);
+  CGX_HIP(hipStreamSynchronize(cg->ctx->stream));
+  const int64_t w = std::min<int64_t>(words, kCoopTraceWords);
+  CGX_HIP(hipMemcpy(host, cg->coop_trace, (size_t)w * 8, hipMemcpyDeviceToHost));
   return CGX_OK;
 }
 

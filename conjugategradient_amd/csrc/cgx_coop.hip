@@ -61,19 +61,36 @@ __device__ __forceinline__ void st_ag(unsigned long long *p, unsigned long long 
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Wave sum in a fixed order on DPP lane moves (no LDS round trips): quad
+// butterflies, the 8- and 16-lane mirrors, then rows 0+1 and 2+3 and their
+// sum into lane 63 (row_bcast15 / row_bcast31). Lanes the moves do not
+// reach add 0.0. The result is read from lane 63.
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RM, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  return v;  // lane 0
+  v += dpp<0xB1>(v);         // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);         // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);        // row_half_mirror: the other quad of 8
+  v += dpp<0x140>(v);        // row_mirror: the other 8 of 16
+  v += dpp<0x142, 0xa>(v);   // row_bcast15: rows 1, 3 add rows 0, 2
+  v += dpp<0x143, 0xc>(v);   // row_bcast31: rows 2, 3 add lane 31
+  return __shfl(v, 63, 64);  // every lane
 }
 
-// fixed-order workgroup sum, valid in thread 0
+// fixed-order workgroup sum of NT threads (every thread gets it); lds: NT / 64
+// slots used by no other block_sum until the next __syncthreads after this one
+template <int NT>
 __device__ __forceinline__ double block_sum(double v, double *lds) {
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
-  const double s = ((lds[0] + lds[1]) + lds[2]) + lds[3];
-  __syncthreads();
+  double s = lds[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) s += lds[w];
   return s;
 }
 
@@ -93,35 +110,41 @@ __device__ __forceinline__ void publish(unsigned long long *gran, double part, u
 // shuffle tree), broadcasts through LDS. false: a spin gave up.
 __device__ __forceinline__ bool collect(const unsigned long long *gran, unsigned tag,
                                         long long ticks, unsigned *tmo, double *res_lds,
-                                        int *ok_lds) {
+                                        int *ok_lds, int nap) {
   const int G = gridDim.x;
+  static_assert(kCoopMaxG <= 128, "collect reads two partials per lane");
   if (threadIdx.x < 64) {
     const int l = threadIdx.x;
     double v = 0.0;
     bool ok = true;
     const long long t0 = wall_clock64();
-    for (int c = 0; c * 64 < G && ok; ++c) {
-      const int w = l + 64 * c;
-      const bool mine = w < G;
-      unsigned long long a = 0, b = 0;
-      for (;;) {
-        bool got = true;
-        if (mine) {
-          a = ld_ag(gran + 2 * w);
-          b = ld_ag(gran + 2 * w + 1);
-          got = (unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag;
-        }
-        if (__all(got)) break;
-        const bool late = wall_clock64() - t0 > ticks ||
-                          __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__any(late)) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    // kCoopMaxG <= 128: lane l holds partials l and l + 64, read in one pass
+    const bool m0 = l < G, m1 = l + 64 < G;
+    unsigned long long a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+    for (;;) {
+      bool got = true;
+      if (m0) {
+        a0 = ld_ag(gran + 2 * l);
+        b0 = ld_ag(gran + 2 * l + 1);
+        got = (unsigned)(a0 >> 32) == tag && (unsigned)(b0 >> 32) == tag;
       }
-      if (ok && mine)
-        v += __longlong_as_double((long long)((a & 0xffffffffull) | ((b & 0xffffffffull) << 32)));
+      if (m1) {
+        a1 = ld_ag(gran + 2 * (l + 64));
+        b1 = ld_ag(gran + 2 * (l + 64) + 1);
+        got = got && (unsigned)(a1 >> 32) == tag && (unsigned)(b1 >> 32) == tag;
+      }
+      if (__all(got)) break;
+      const bool late = wall_clock64() - t0 > ticks ||
+                        __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__any(late)) {
+        ok = false;
+        break;
+      }
+      for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(1);
+    }
+    if (ok) {
+      if (m0) v = __longlong_as_double((long long)((a0 & 0xffffffffull) | ((b0 & 0xffffffffull) << 32)));
+      if (m1) v += __longlong_as_double((long long)((a1 & 0xffffffffull) | ((b1 & 0xffffffffull) << 32)));
     }
     v = wave_sum(v);
     if (l == 0) {
@@ -136,46 +159,116 @@ __device__ __forceinline__ bool collect(const unsigned long long *gran, unsigned
 
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <int R>
-__global__ __launch_bounds__(kBlock, 1) void k_cg_coop(
-    int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
-    const double *__restrict__ val, double *__restrict__ x, double *r, double *p0, double *p1,
-    CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks) {
-  __shared__ double red[4];
-  __shared__ double res;
-  __shared__ int okf;
-  if (!st->active[slot0]) return;  // the same word for every workgroup
-  const int t = threadIdx.x;
-  double rxr = st->rxr[slot0];
-  const double tol = st->tol;
-  const long long cap = st->cap;
-  long long bodies = st->bodies;
-
-  int64_t row[R], rb[R];
-  int cnt[R];
-  int cc[R][kCoopK];
-  double cv[R][kCoopK];
-  double xr[R], rv[R], pv[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    row[u] = ((int64_t)blockIdx.x * R + u) * kBlock + t;
-    const bool ok = row[u] < n;
-    rb[u] = ok ? rowptr[row[u]] : 0;
-    cnt[u] = ok ? rowptr[row[u] + 1] - (int)rb[u] : 0;
-#pragma unroll
-    for (int k = 0; k < kCoopK; ++k) {
-      cc[u][k] = k < cnt[u] ? col[rb[u] + k] : 0;
-      cv[u][k] = k < cnt[u] ? val[rb[u] + k] : 0.0;
+// One entry of a tagged vector copy: two {tag, half} granules per entry,
+// each written by one 8-byte atomic store (the data is the flag, MI355X guide
+// §6 Guideline 16 R2). ld_tagged re-reads until both halves carry `tag`
+// (bounded; on timeout it raises tmo and returns 0).
+__device__ __forceinline__ void st_tagged(unsigned long long *g, int64_t j, double v,
+                                          unsigned tag) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long hi = (unsigned long long)tag << 32;
+  st_ag(g + 2 * j, hi | (u & 0xffffffffull));
+  st_ag(g + 2 * j + 1, hi | (u >> 32));
+}
+__device__ __forceinline__ double untag(unsigned long long a, unsigned long long b) {
+  return __longlong_as_double((long long)((a & 0xffffffffull) | ((b & 0xffffffffull) << 32)));
+}
+__device__ __forceinline__ bool tagged(unsigned long long a, unsigned long long b, unsigned tag) {
+  return (unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag;
+}
+__device__ __forceinline__ double ld_tagged(const unsigned long long *g, int64_t j, unsigned tag,
+                                            long long t0, long long ticks, unsigned *tmo) {
+  for (;;) {
+    const unsigned long long a = ld_ag(g + 2 * j), b = ld_ag(g + 2 * j + 1);
+    if (tagged(a, b, tag)) return untag(a, b);
+    if (wall_clock64() - t0 > ticks ||
+        __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0.0;
     }
-    xr[u] = ok ? x[row[u]] : 0.0;
-    rv[u] = ok ? r[row[u]] : 0.0;
-    pv[u] = ok ? p0[row[u]] : 0.0;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Diagnostics ($CGX_COOP_TRACE, cgx_cg_coop_trace): thread 0 of every
+// workgroup stamps the wall clock at the phases of bodies 8-15 of a launch
+#define CGX_COOP_TR(ph)                                                                  \
+  if (trace && i >= 8 && i < 16 && t == 0)                                               \
+    trace[((size_t)blockIdx.x * 8 + (i - 8)) * 8 + (ph)] = wall_clock64();
+
+// Shared prologue: this thread's rows, their first kCoopK entries, x, r, p.
+#define CGX_COOP_PROLOGUE                                                        \
+  __shared__ double red[2][NT / 64]; /* [exchange A / B] */                      \
+  __shared__ double res;                                                         \
+  __shared__ int okf;                                                            \
+  if (!st->active[slot0]) return; /* the same word for every workgroup */        \
+  const int t = threadIdx.x;                                                     \
+  double rxr = st->rxr[slot0];                                                   \
+  const double tol = st->tol;                                                    \
+  const long long cap = st->cap;                                                 \
+  long long bodies = st->bodies;                                                 \
+  int64_t row[R], rb[R];                                                         \
+  int cnt[R];                                                                    \
+  int cc[R][kCoopK];                                                             \
+  double cv[R][kCoopK];                                                          \
+  double xr[R], rv[R], pv[R];                                                    \
+  _Pragma("unroll") for (int u = 0; u < R; ++u) {                                \
+    row[u] = ((int64_t)blockIdx.x * R + u) * NT + t;                             \
+    const bool ok = row[u] < n;                                                  \
+    rb[u] = ok ? rowptr[row[u]] : 0;                                             \
+    cnt[u] = ok ? rowptr[row[u] + 1] - (int)rb[u] : 0;                           \
+    _Pragma("unroll") for (int k = 0; k < kCoopK; ++k) {                         \
+      cc[u][k] = k < cnt[u] ? col[rb[u] + k] : 0;                                \
+      cv[u][k] = k < cnt[u] ? val[rb[u] + k] : 0.0;                              \
+    }                                                                            \
+    xr[u] = ok ? x[row[u]] : 0.0;                                                \
+    rv[u] = ok ? r[row[u]] : 0.0;                                                \
+    pv[u] = ok ? p0[row[u]] : 0.0;                                               \
   }
 
+// The body's record and stop rule, as k_update_xp (CG.hpp:396-404, 436);
+// returns cont
+__device__ __forceinline__ bool coop_record(CgScalars<double> *st, int s, double pAp, double rr,
+                                            double alpha, double rxr, double tol,
+                                            long long bodies, long long cap) {
+  const bool cond = isnan(rxr) || sqrt(rxr) <= tol;
+  const bool cont = !cond && bodies < cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by the host after the launch
+    st->pAp[s] = pAp;
+    st->rr[s] = rr;
+    st->alpha[s] = alpha;
+    st->rxr[(s + 1) & 3] = rr;
+    st->bodies = bodies;
+    st->stopped = cond ? 1 : (cont ? 0 : 2);
+    st->active[(s + 1) & 3] = cont ? 1 : 0;
+    if (!cont)
+      for (int q = 0; q < 4; ++q) st->active[q] = 0;
+  }
+  return cont;
+}
+
+__device__ __forceinline__ void coop_gave_up(CgScalars<double> *st) {
+  if (threadIdx.x == 0) {  // a spin gave up (okf == 0 in every workgroup that gets here)
+    st->stopped = 4;
+    for (int q = 0; q < 4; ++q) st->active[q] = 0;
+  }
+}
+
+// Form 0 (write-through, $CGX_COOP_TAGR=0): r and p_k stored with agent-scope
+// stores (sc1) into r and p0 / p1, every storing wave drained before its
+// workgroup publishes; the gathers of a body run after both exchanges.
+template <int R, int NT>
+__global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
+    int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, double *__restrict__ x, double *r, double *p0, double *p1,
+    CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks,
+    unsigned long long *trace, int nap) {
+  CGX_COOP_PROLOGUE
   double beta = 0.0;
   for (int i = 0; i < m; ++i) {
     const int s = (slot0 + i) & 3;
     const unsigned tag = (unsigned)i + 1u;
+    CGX_COOP_TR(0)
     double *pcur = (i & 1) ? p1 : p0;         // p_k of this body (own rows stored here)
     const double *pprev = (i & 1) ? p0 : p1;  // p_{k-1}: the previous body's buffer
     double q[R];
@@ -211,14 +304,17 @@ __global__ __launch_bounds__(kBlock, 1) void k_cg_coop(
         q[u] = acc;
       }
     }
+    CGX_COOP_TR(1)
     // p.Ap (CG.hpp:374-379)
     double part = 0.0;
 #pragma unroll
     for (int u = 0; u < R; ++u) part += pv[u] * q[u];
     drain();  // this wave's p stores are out before the workgroup publishes
-    part = block_sum(part, red);
+    part = block_sum<NT>(part, red[0]);
+    CGX_COOP_TR(2)
     publish(cw->ga, part, tag);
-    if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf)) break;
+    if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(3)
     const double pAp = res;
     const double alpha = rxr / pAp;
     // x += alpha p; r -= alpha Ap; r.r   (CG.hpp:381-393, 406-407)
@@ -231,77 +327,208 @@ __global__ __launch_bounds__(kBlock, 1) void k_cg_coop(
       part += rv[u] * rv[u];
     }
     drain();
-    part = block_sum(part, red);
+    part = block_sum<NT>(part, red[1]);
+    CGX_COOP_TR(4)
     publish(cw->gb, part, tag);
-    if (!collect(cw->gb, tag, ticks, &cw->tmo, &res, &okf)) break;
+    CGX_COOP_TR(5)
+    if (!collect(cw->gb, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(6)
     const double rr = res;
-    // stop rule, as k_update_xp (CG.hpp:396-404, 436)
     ++bodies;
-    const bool cond = isnan(rxr) || sqrt(rxr) <= tol;
-    const bool cont = !cond && bodies < cap;
+    const bool cont = coop_record(st, s, pAp, rr, alpha, rxr, tol, bodies, cap);
     beta = rr / rxr;
-    if (blockIdx.x == 0 && t == 0) {  // the record (read by the host after the launch)
-      st->pAp[s] = pAp;
-      st->rr[s] = rr;
-      st->alpha[s] = alpha;
-      st->rxr[(s + 1) & 3] = rr;
-      st->bodies = bodies;
-      st->stopped = cond ? 1 : (cont ? 0 : 2);
-      st->active[(s + 1) & 3] = cont ? 1 : 0;
-      if (!cont)
-        for (int q2 = 0; q2 < 4; ++q2) st->active[q2] = 0;
-    }
     rxr = rr;
     if (!cont || i == m - 1) {
-      // p_{k+1} = r + beta p, and x, into the standard buffers
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         if (row[u] < n) {
-          p0[row[u]] = rv[u] + beta * pv[u];
+          p0[row[u]] = rv[u] + beta * pv[u];  // p_{k+1}, and x, in the standard buffers
           x[row[u]] = xr[u];
         }
       }
       return;
     }
   }
-  // a spin gave up (okf == 0 in every workgroup that reaches here)
-  if (t == 0) {
-    st->stopped = 4;
-    for (int q2 = 0; q2 < 4; ++q2) st->active[q2] = 0;
+  coop_gave_up(st);
+}
+
+// Form 1 (tagged, the default): p_k and r_{k+1} are handed over as tagged
+// granules (pg: two copies of 2 n words, body k in copy k mod 2; rg: 2 n
+// words; all zeroed before the launch), so no exchange waits for a drain,
+// and the next body's gathers are issued right after this body's r.r
+// partial is published: they overlap the r.r exchange (a gatherer that
+// finds a stale tag re-reads, bounded). Same values as form 0.
+template <int R, int NT>
+__global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
+    int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, double *__restrict__ x, double *r, double *p0,
+    unsigned long long *pg, unsigned long long *rg, CgScalars<double> *st, int slot0, int m,
+    CoopWs *cw, long long ticks, unsigned long long *trace, int nap) {
+  CGX_COOP_PROLOGUE
+  double gp[R][kCoopK], gr[R][kCoopK];  // this body's gathered p_{k-1}[j] (body 0: p_k) and r_k[j]
+#pragma unroll
+  for (int u = 0; u < R; ++u)
+#pragma unroll
+    for (int k = 0; k < kCoopK; ++k) {
+      gp[u][k] = k < cnt[u] ? ld_ag(p0 + cc[u][k]) : 0.0;
+      gr[u][k] = 0.0;
+    }
+  double beta = 0.0;
+  for (int i = 0; i < m; ++i) {
+    const int s = (slot0 + i) & 3;
+    const unsigned tag = (unsigned)i + 1u;
+    CGX_COOP_TR(0)
+    unsigned long long *pgc = pg + (size_t)(i & 1) * 2 * n;  // p_k, tag i + 1
+    const unsigned long long *pgp = pg + (size_t)((i + 1) & 1) * 2 * n;  // p_{k-1}, tag i
+    double q[R];
+    if (i > 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) pv[u] = rv[u] + beta * pv[u];  // CG.hpp:418, own rows
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (row[u] < n) st_tagged(pgc, row[u], pv[u], tag);
+    const long long t0 = wall_clock64();
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      double acc = 0.0;
+      if (i == 0) {
+#pragma unroll
+        for (int k = 0; k < kCoopK; ++k)
+          if (k < cnt[u]) acc += cv[u][k] * gp[u][k];
+        for (int k = kCoopK; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kCoopK; ++k)
+          if (k < cnt[u]) acc += cv[u][k] * (gr[u][k] + beta * gp[u][k]);
+        for (int k = kCoopK; k < cnt[u]; ++k) {
+          const int j = col[rb[u] + k];
+          acc += val[rb[u] + k] * (ld_tagged(rg, j, (unsigned)i, t0, ticks, &cw->tmo) +
+                                   beta * ld_tagged(pgp, j, (unsigned)i, t0, ticks, &cw->tmo));
+        }
+      }
+      q[u] = acc;
+    }
+    CGX_COOP_TR(1)
+    // p.Ap (CG.hpp:374-379)
+    double part = 0.0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) part += pv[u] * q[u];
+    part = block_sum<NT>(part, red[0]);
+    CGX_COOP_TR(2)
+    publish(cw->ga, part, tag);
+    if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(3)
+    const double pAp = res;
+    const double alpha = rxr / pAp;
+    // x += alpha p; r -= alpha Ap; r.r   (CG.hpp:381-393, 406-407)
+    part = 0.0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      xr[u] = xr[u] + alpha * pv[u];
+      rv[u] = rv[u] - alpha * q[u];
+      if (row[u] < n) st_tagged(rg, row[u], rv[u], tag);
+      part += rv[u] * rv[u];
+    }
+    part = block_sum<NT>(part, red[1]);
+    CGX_COOP_TR(4)
+    publish(cw->gb, part, tag);
+    if (i < m - 1) {
+      // the next body's gathers: p_k[j] (tag i + 1, stored above by every
+      // workgroup) and r_{k+1}[j] (tag i + 1, stored after the p.Ap exchange)
+      const long long t1 = wall_clock64();
+      bool bad = false;
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+#pragma unroll
+        for (int k = 0; k < kCoopK; ++k)
+          if (k < cnt[u]) {
+            const int j = cc[u][k];
+            const unsigned long long a = ld_ag(pgc + 2 * j), b = ld_ag(pgc + 2 * j + 1);
+            const unsigned long long c = ld_ag(rg + 2 * j), d = ld_ag(rg + 2 * j + 1);
+            bad |= !tagged(a, b, tag) || !tagged(c, d, tag);
+            gp[u][k] = untag(a, b);
+            gr[u][k] = untag(c, d);
+          }
+      if (__any(bad)) {  // stores not landed yet: re-read until they have
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+#pragma unroll
+          for (int k = 0; k < kCoopK; ++k)
+            if (k < cnt[u]) {
+              gp[u][k] = ld_tagged(pgc, cc[u][k], tag, t1, ticks, &cw->tmo);
+              gr[u][k] = ld_tagged(rg, cc[u][k], tag, t1, ticks, &cw->tmo);
+            }
+      }
+    }
+    CGX_COOP_TR(5)
+    if (!collect(cw->gb, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(6)
+    const double rr = res;
+    ++bodies;
+    const bool cont = coop_record(st, s, pAp, rr, alpha, rxr, tol, bodies, cap);
+    beta = rr / rxr;
+    rxr = rr;
+    if (!cont || i == m - 1) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (row[u] < n) {
+          p0[row[u]] = rv[u] + beta * pv[u];  // p_{k+1}, x and r in the standard buffers
+          x[row[u]] = xr[u];
+          r[row[u]] = rv[u];
+        }
+      }
+      return;
+    }
   }
+  coop_gave_up(st);
 }
 
 }  // namespace
 
-int coop_rows_per_thread(int64_t n, int want) {
+int coop_rows_per_thread(int64_t n, int want, int nt) {
   static const int opts[] = {1, 2, 4};
+  if (nt != 256 && nt != 512 && nt != 1024) return 0;
   for (int R : opts) {
     if (want > 0 && R != want) continue;
-    if ((n + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R) <= kCoopMaxG) return R;
+    if (nt > 256 && R != 1) continue;
+    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= kCoopMaxG) return R;
   }
   return 0;
 }
 
-hipError_t cg_coop(int64_t n, int R, const int *rowptr, const int *col, const double *val,
-                   double *x, double *r, double *p0, double *p1, CgScalars<double> *st, int slot0,
-                   int m, CoopWs *cw, long long ticks, hipStream_t s) {
-  const int G = (int)((n + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R));
-  if (G < 1 || G > kCoopMaxG || m < 1) return hipErrorInvalidValue;
+hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
+                   const double *val, double *x, double *r, double *p0, double *p1,
+                   unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
+                   long long ticks, unsigned long long *trace, int nap, hipStream_t s) {
+  const int G = (int)((n + (int64_t)NT * R - 1) / ((int64_t)NT * R));
+  if (G < 1 || G > kCoopMaxG || m < 1 || (tagged && !g)) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
+  if (e == hipSuccess && tagged) e = hipMemsetAsync(g, 0, (size_t)n * 48, s);
   if (e != hipSuccess) return e;
-  switch (R) {
-    case 1:
-      k_cg_coop<1><<<G, kBlock, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, ticks);
-      break;
-    case 2:
-      k_cg_coop<2><<<G, kBlock, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, ticks);
-      break;
-    case 4:
-      k_cg_coop<4><<<G, kBlock, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, ticks);
-      break;
-    default:
-      return hipErrorInvalidValue;
+  unsigned long long *pg = g, *rg = g ? g + 4 * n : nullptr;
+#define CGX_COOP_WT(RR, TT)                                                                 \
+  k_cg_coop_wt<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
+                                        ticks, trace, nap)
+#define CGX_COOP_TG(RR, TT)                                                                 \
+  k_cg_coop_tg<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, pg, rg, st, slot0, m, \
+                                        cw, ticks, trace, nap)
+  const int key = (NT == 1024 ? 100 : NT == 512 ? 50 : 0) + R * 2 + (tagged ? 1 : 0);
+  switch (key) {
+    case 2: CGX_COOP_WT(1, 256); break;
+    case 3: CGX_COOP_TG(1, 256); break;
+    case 4: CGX_COOP_WT(2, 256); break;
+    case 5: CGX_COOP_TG(2, 256); break;
+    case 8: CGX_COOP_WT(4, 256); break;
+    case 9: CGX_COOP_TG(4, 256); break;
+    case 52: CGX_COOP_WT(1, 512); break;
+    case 53: CGX_COOP_TG(1, 512); break;
+    case 102: CGX_COOP_WT(1, 1024); break;
+    case 103: CGX_COOP_TG(1, 1024); break;
+    default: return hipErrorInvalidValue;
   }
+#undef CGX_COOP_WT
+#undef CGX_COOP_TG
   return hipGetLastError();
 }
 

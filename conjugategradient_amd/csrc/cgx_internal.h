@@ -274,14 +274,20 @@ struct CoopWs {
   unsigned int pad[3];
 };
 // rows per thread (1, 2 or 4; `want` > 0 asks for one) for which n rows fit
-// kCoopMaxG workgroups; 0: none
-int coop_rows_per_thread(int64_t n, int want);
+// kCoopMaxG workgroups of nt threads (256, or 1024 with one row per
+// thread); 0: none
+int coop_rows_per_thread(int64_t n, int want, int nt);
 // up to m bodies from slot0 in one launch (f64, single device): x, r, p0 in
 // and out in the standard layout, p1 scratch (n entries); stops as the
 // three-kernel body does, or sets st->stopped = 4 when a spin gave up
-hipError_t cg_coop(int64_t n, int R, const int *rowptr, const int *col, const double *val,
-                   double *x, double *r, double *p0, double *p1, CgScalars<double> *st, int slot0,
-                   int m, CoopWs *cw, long long ticks, hipStream_t s);
+// tagged (form 1): p and r handed over as tagged granules in g (6 n words:
+// two p copies, then r), else (form 0) drained write-through stores into r,
+// p0 and p1
+hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
+                   const double *val, double *x, double *r, double *p0, double *p1,
+                   unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
+                   long long ticks, unsigned long long *trace, int nap, hipStream_t s);
+constexpr int kCoopTraceWords = kCoopMaxG * 8 * 8;  // workgroups x bodies 8-15 x phases
 
 // value-code templates (cgx_abi.cpp build_value_templates): per slice the
 // hash of its 4-bit code chunk (0: wider than one chunk); the template slice

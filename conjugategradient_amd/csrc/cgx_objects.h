@@ -183,7 +183,12 @@ struct cgx_cg {
   bool fdefer = false;  // mode 4: p update folded into the SpMV, x deferred as mode 3
   bool coop = false;    // mode 5: persistent body, one launch per chunk (cgx_coop.hip)
   int coop_r = 0;       // its rows per thread
+  int coop_nt = 1024;   // threads per workgroup ($CGX_COOP_NT: 256, 512 or 1024)
+  int coop_nap = 1;     // s_sleep(1)s per exchange poll ($CGX_COOP_NAP)
   void *coop_ws = nullptr;  // cgx::CoopWs
+  void *coop_rg = nullptr;  // tagged p and r granules (6 n words; $CGX_COOP_TAGR=1)
+  bool coop_tagr = false;
+  void *coop_trace = nullptr;  // $CGX_COOP_TRACE: phase stamps (cgx_cg_coop_trace)
   long long coop_ticks = 0; // wall-clock ticks before an exchange spin gives up
   bool altdir = false;  // alternate the kernels' sweep directions (Infinity-Cache reuse)
   void *pk[3] = {nullptr, nullptr, nullptr};  // p buffers 1..3 of mode 3 (n + n_ghost)

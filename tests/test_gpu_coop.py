@@ -70,8 +70,11 @@ def test_mode5_solves_to_tolerance_and_warm_start(queue, oracle):
 
 def test_mode5_irregular_rows(queue, oracle):
     """Rows longer than the kCoopK entries held in registers (a hub row of
-    300 entries) read their tail from the CSR arrays."""
-    rp, cl, vl = irregular_spd(20000, hub=300)
+    300 entries) read their tail from the CSR arrays. Diagonal shift 10: a
+    well-conditioned system, where 30 bodies in two summation orders agree to
+    1e-15 on the CPU (with the stand-in's shift of 1e-2 the oracle's own 1-
+    and 8-thread runs differ by 5e-3 after 30 bodies on this hub matrix)."""
+    rp, cl, vl = irregular_spd(20000, seed=4, hub=300, shift=10.0)
     assert np.diff(rp).max() > 8
     m = cga.Matrix(queue, vl, cl, rp)
     b = np.arange(1, len(rp), dtype=np.float64)
@@ -112,3 +115,23 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
         assert L.cgx_cg_set_mode(h, 5) != 0
     finally:
         L.cgx_cg_destroy(h)
+
+
+@pytest.mark.parametrize("tagr", ["0", "1"])
+def test_mode5_r_handoff_forms(queue, oracle, monkeypatch, tagr):
+    """r handed over as tagged granules (default) or as drained write-through
+    stores ($CGX_COOP_TAGR=0): the same values bit for bit (only the
+    hand-off differs), matching the oracle."""
+    monkeypatch.setenv("CGX_COOP_TAGR", tagr)
+    rp, cl, vl = oracle.poisson(2, 128, 128, 1)
+    n = len(rp) - 1
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    x5, it5, r5 = _solve(queue, m, b, 5, 0.0, max_iter=60, poll=4)
+    monkeypatch.setenv("CGX_COOP_TAGR", "1" if tagr == "0" else "0")
+    x5b, it5b, r5b = _solve(queue, m, b, 5, 0.0, max_iter=60, poll=4)
+    assert it5 == it5b == 60
+    np.testing.assert_array_equal(x5, x5b)
+    assert r5 == r5b
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 60, 8)
+    assert rel(x5, xr) <= 1e-10

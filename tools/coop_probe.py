@@ -18,9 +18,15 @@ from conjugategradient_amd import workloads  # noqa: E402
 CONFIGS = {
     "p2d_128": lambda: ("poisson", (2, 128, 128, 1)),
     "p2d_256": lambda: ("poisson", (2, 256, 256, 1)),
+    "p2d_64": lambda: ("poisson", (2, 64, 64, 1)),
+    "p2d_180": lambda: ("poisson", (2, 180, 180, 1)),
+    "p3d_32": lambda: ("poisson", (3, 32, 32, 32)),
     "p3d_40": lambda: ("poisson", (3, 40, 40, 40)),
     "irr_100k": lambda: ("irr", 100000),
 }
+
+
+VARIANTS = [(0, None, None, None), (5, "1", "0", "1024"), (5, "1", "0", "512"), (5, "1", "1", "512")]
 
 
 def main():
@@ -45,9 +51,11 @@ def main():
         b = torch.arange(1, n + 1, dtype=torch.float64, device="cuda")
         res = {}
         for rnd in range(a.rounds):
-            for mode, R in ((0, None), (5, "1"), (5, "2"), (5, "4")):
+            for mode, R, tg, nt in VARIANTS:
                 if R:
                     os.environ["CGX_COOP_R"] = R
+                    os.environ["CGX_COOP_TAGR"] = tg
+                    os.environ["CGX_COOP_NT"] = nt
                 x = torch.zeros(n, dtype=torch.float64, device="cuda")
                 torch.cuda.synchronize()
                 cg = C.c_void_p()
@@ -70,10 +78,12 @@ def main():
                 rxr = C.c_double()
                 check(L.cgx_cg_rxr(cg, C.byref(rxr)))
                 check(L.cgx_cg_destroy(cg))
-                key = (mode if mode != 5 else f"5/R{R}")
+                key = (mode if mode != 5 else f"5/R{R}/tagr{tg}/nt{nt}")
                 ran = bodies.value - a.warmup
                 res.setdefault(key, []).append((dt / max(ran, 1) * 1e6, ran, me.value, rxr.value))
                 os.environ.pop("CGX_COOP_R", None)
+                os.environ.pop("CGX_COOP_TAGR", None)
+                os.environ.pop("CGX_COOP_NT", None)
         for k, v in res.items():
             us = sorted(t[0] for t in v)
             print(json.dumps({"config": name, "n": n, "mode": k, "mode_eff": v[0][2], "bodies": v[0][1],
