@@ -77,7 +77,7 @@ def update_bytes_per_iter(n: int, mode: int) -> int:
     +40 n), 34 n on average."""
     if mode == 4:  # the p update is folded into the SpMV (spmv_bytes_per_iter);
         return 24 * n + 12 * n  # the slot-3 x flush: x r/w + 4 p reads, once per 4 bodies
-    xp = 40 * n if mode == 1 else 34 * n
+    xp = 40 * n if mode in (1, 5) else 34 * n  # mode 5: priced as mode 1
     return 24 * n + xp
 
 
@@ -114,7 +114,7 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
-    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4], default=0,
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4, 5], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
                          "2 fused (single GPU), 3 three kernels with the x update deferred, "
                          "4 two kernels (p update folded into the SpMV), x deferred")
@@ -424,7 +424,9 @@ def run(args) -> None:
         check(L.cgx_cg_run(cg, args.profile_steps, C.byref(bodies), C.byref(stopped)))
         check(L.cgx_cg_kernel_times(cg, avg, calls))
         check(L.cgx_cg_set_kernel_timing(cg, 0))
-    if calls[1] > 0:
+    if calls[1] > 0 and mode_eff == 5:
+        roof = coop_roofline(L, cg, avg, calls, args.profile_steps, iter_local)
+    elif calls[1] > 0:
         kb = spmv_fmt_local + (32 * n_local if fused else 0)
         ach = kb / (avg[1] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
@@ -460,7 +462,10 @@ def run(args) -> None:
 
     # ---- general-value formats on the same matrix (N = 1) --------------------------
     general = None
-    if world == 1 and rank == 0 and not args.no_general:
+    if world == 1 and rank == 0 and not args.no_general and mode_eff == 5:
+        general = {"skipped": "mode 5 (persistent body) reads the CSR arrays directly; the "
+                              "SpMV formats do not enter it"}
+    elif world == 1 and rank == 0 and not args.no_general:
         general = general_formats(L, q, A, b, x, n_local, nnz_local, mode_eff, args)
 
     line = None
@@ -505,7 +510,9 @@ def run(args) -> None:
                        "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies",
                                      4: "2 kernels (p update in the SpMV), x update deferred "
-                                        "over 4 bodies"}[mode_eff] +
+                                        "over 4 bodies",
+                                     5: "persistent body (one launch per chunk of bodies, two "
+                                        "grid-wide exchanges per body)"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
                        "spmv_variant": int(variant.value),
                        "value_code_templates": (
@@ -523,6 +530,31 @@ def run(args) -> None:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def coop_roofline(L, cg, avg, calls, bodies: int, iter_bytes: int) -> dict:
+    """Mode 5 runs the whole body in one persistent kernel (k_cg_coop_wt or
+    _tg), so the kernel's line is the iteration's: compulsory bytes of a
+    body (as mode 1 moves them) over the HIP-event time per body. The body
+    is latency-bound (two grid-wide exchanges, one gather round trip); its
+    vectors stay in the L2s and the Infinity Cache, so no HBM traffic is
+    claimed (PMC FETCH_SIZE would count the exchanges' L2-bypassing loads)."""
+    R, NT, G, T = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(L.cgx_cg_coop_shape(cg, C.byref(R), C.byref(NT), C.byref(G), C.byref(T)))
+    t_launch = avg[1] * 1e-3
+    t_body = t_launch * calls[1] / max(bodies, 1)
+    ach = iter_bytes / t_body / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": f"k_cg_coop_{'tg' if T.value else 'wt'}",
+            "template": f"<{R.value}, {NT.value}>", "workgroups": G.value,
+            "bytes_per_launch": int(iter_bytes * bodies / max(calls[1], 1)),
+            "bytes_basis": "compulsory bytes of a body as the three-kernel body moves them "
+                           "(matrix stream + 16 n SpMV + 64 n updates) x bodies per launch",
+            "avg_us": round(avg[1] * 1e3, 2), "launches_timed": int(calls[1]),
+            "us_per_body": round(t_body * 1e6, 3),
+            "traffic_note": "latency-bound persistent body: vectors L2 / Infinity-Cache "
+                            "resident, no HBM traffic claimed"}
 
 
 def kernel_base_name(full: str) -> str:

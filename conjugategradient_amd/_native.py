@@ -89,7 +89,8 @@ _SIGS = {
     "cgx_cg_kernel_times": (_i32, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "cgx_cg_config": (_i32, [_vp, _i32, _i32]),
     "cgx_cg_set_mode": (_i32, [_vp, _i32]),
-    "cgx_cg_coop_shape": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
+    "cgx_cg_coop_shape": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
+                                 C.POINTER(_i32)]),
     "cgx_cg_coop_trace": (_i32, [_vp, C.POINTER(C.c_uint64), _i64]),
     "cgx_cg_get_mode": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_fd_grid": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),

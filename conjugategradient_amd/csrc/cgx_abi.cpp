@@ -1944,21 +1944,44 @@ static bool fd_auto(const cgx_cg *cg) {
   return march2d || (small && (v & 1048576));
 }
 
+// Auto mode picks 5 (the persistent body) for small single-device f64
+// problems whose rows hold at most kCoopK entries: one workgroup of 1024
+// threads per 1024 rows, at most kCoopMaxG of them (profiles/r03_coop_*.log:
+// 128^2 5.97 against 9.61 us per body in mode 4, 256^2 6.9 against 10.0,
+// 40^3 8.0 against 10.6; an irregular 100k-row matrix with longer rows
+// ties, 14.8 against 14.9 in mode 3).
+static bool coop_auto(const cgx_cg *cg) {
+  const cgx_csr *A = cg->A;
+  if (A->dist || cg->dtype != CGX_F64) return false;
+  if (const char *e = std::getenv("CGX_AUTO_COOP")) {
+    if (std::atoi(e) == 0) return false;
+  }
+  return A->max_row_nnz <= kCoopK && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1;
+}
+
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
   CGX_REQUIRE(mode >= 0 && mode <= 5, CGX_EINVAL,
               "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
               "4 fused with deferred x, 5 persistent body", mode);
   int coop_r = 0;
+  if (!cg->begun) {  // mode 5's shape knobs (A/B; the defaults are the measured best)
+    cg->coop_nt = 1024;
+    cg->coop_nap = 1;
+    cg->coop_tagr = false;
+    if (const char *e = std::getenv("CGX_COOP_NT")) cg->coop_nt = std::atoi(e);
+    if (const char *e = std::getenv("CGX_COOP_NAP")) cg->coop_nap = std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
+  }
   if (mode == 5) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) runs f64 on a single device");
-    if (const char *e = std::getenv("CGX_COOP_NT")) cg->coop_nt = std::atoi(e);
-    if (const char *e = std::getenv("CGX_COOP_NAP")) cg->coop_nap = std::max(0, std::atoi(e));
     coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
     CGX_REQUIRE(coop_r > 0, CGX_EUNSUPPORTED,
-                "mode 5 (persistent body) takes at most %lld rows (n = %lld)",
-                (long long)kCoopMaxG * kBlock * 4, (long long)cg->n);
+                "mode 5 (persistent body) takes at most %lld rows with %d threads per "
+                "workgroup (n = %lld)",
+                (long long)kCoopMaxG * cg->coop_nt * (cg->coop_nt == 256 ? 4 : 1),
+                cg->coop_nt, (long long)cg->n);
   }
   CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
               "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
@@ -1969,7 +1992,11 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(mode != 4 || (cg->dtype == CGX_F64 && Launch<double>::fd_supported(cg->A->dev)),
               CGX_EUNSUPPORTED, "mode 4 needs an f64 matrix in a production SpMV format "
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
-  if (mode == 0) mode = fd_auto(cg) ? 4 : 3;
+  if (mode == 0) {
+    mode = coop_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
+    if (mode == 5) coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
+    if (mode == 5 && coop_r == 0) mode = fd_auto(cg) ? 4 : 3;
+  }
   const bool f = mode == 2, d = mode == 3, fd = mode == 4, c = mode == 5;
   if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop) {
     CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
@@ -1979,7 +2006,6 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     DeviceGuard g(cg->ctx->device);
     CGX_HIP(hipMalloc(&cg->coop_ws, sizeof(CoopWs)));
     CGX_HIP(hipMalloc(&cg->coop_rg, (size_t)cg->n * 48));
-    if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
     if (const char *e = std::getenv("CGX_COOP_TRACE"); e && std::atoi(e)) {
       CGX_HIP(hipMalloc(&cg->coop_trace, kCoopTraceWords * sizeof(unsigned long long)));
       CGX_HIP(hipMemset(cg->coop_trace, 0, kCoopTraceWords * sizeof(unsigned long long)));
@@ -2246,11 +2272,13 @@ extern "C" int cgx_cg_prepare(cgx_cg *cg, int64_t bodies) {
   return CGX_OK;
 }
 
-extern "C" int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *workgroups,
-                                 int *tagged) {
-  CGX_REQUIRE(cg && rows_per_thread && workgroups && tagged, CGX_EINVAL, "NULL argument");
+extern "C" int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads,
+                                 int *workgroups, int *tagged) {
+  CGX_REQUIRE(cg && rows_per_thread && threads && workgroups && tagged, CGX_EINVAL,
+              "NULL argument");
   CGX_REQUIRE(cg->coop, CGX_ESTATE, "the solver is not in mode 5");
   *rows_per_thread = cg->coop_r;
+  *threads = cg->coop_nt;
   const int64_t per = (int64_t)cg->coop_nt * cg->coop_r;
   *workgroups = (int)((cg->n + per - 1) / per);
   *tagged = cg->coop_tagr ? 1 : 0;

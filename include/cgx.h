@@ -194,9 +194,11 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
  * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
-/* mode 5's launch shape: rows per thread, workgroups, 1 when p and r are
- * handed over as tagged granules ($CGX_COOP_TAGR, default 1) */
-int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *workgroups, int *tagged);
+/* mode 5's launch shape: rows per thread, threads per workgroup ($CGX_COOP_NT,
+ * default 1024), workgroups, 1 when p and r are handed over as tagged
+ * granules ($CGX_COOP_TAGR=1; default 0: drained write-through stores) */
+int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads, int *workgroups,
+                      int *tagged);
 /* diagnostics: with $CGX_COOP_TRACE=1 set before mode 5 is chosen, the
  * wall-clock stamps (100 MHz) of the last launch: [workgroup][body 8..15]
  * [phase 0..7] (0 body start, 1 SpMV done, 2 p.Ap partial ready, 3 p.Ap

@@ -29,11 +29,18 @@ def _solve(queue, m, b, mode, tol, max_iter=-1, x0=None, poll=32):
     return cg.extract(), cg.iterations, cg.final_rxr
 
 
-@pytest.mark.parametrize("R", ["1", "2", "4"])
+SHAPES = [("1", "256", "0"), ("2", "256", "0"), ("4", "256", "0"), ("1", "512", "0"),
+          ("1", "1024", "0"), ("1", "256", "1"), ("2", "256", "1"), ("1", "512", "1")]
+
+
+@pytest.mark.parametrize("R,NT,tagged", SHAPES, ids=["-".join(s) for s in SHAPES])
 @pytest.mark.parametrize("dims", [(2, 128, 128, 1), (3, 20, 18, 17), (2, 70, 66, 1)],
                          ids=["p2d_128", "p3d_20x18x17", "p2d_70x66"])
-def test_mode5_fixed_bodies_match_oracle(queue, oracle, monkeypatch, dims, R):
+def test_mode5_fixed_bodies_match_oracle(queue, oracle, monkeypatch, dims, R, NT, tagged):
+    """rows per thread x threads per workgroup x hand-off form"""
     monkeypatch.setenv("CGX_COOP_R", R)
+    monkeypatch.setenv("CGX_COOP_NT", NT)
+    monkeypatch.setenv("CGX_COOP_TAGR", tagged)
     rp, cl, vl = oracle.poisson(*dims)
     n = len(rp) - 1
     m = cga.Matrix(queue, vl, cl, rp)
@@ -119,9 +126,10 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
 
 @pytest.mark.parametrize("tagr", ["0", "1"])
 def test_mode5_r_handoff_forms(queue, oracle, monkeypatch, tagr):
-    """r handed over as tagged granules (default) or as drained write-through
-    stores ($CGX_COOP_TAGR=0): the same values bit for bit (only the
-    hand-off differs), matching the oracle."""
+    """p and r handed over as drained write-through stores (default) or as
+    tagged granules with the next body's gathers overlapping the r.r exchange
+    ($CGX_COOP_TAGR=1): the same values bit for bit (only the hand-off
+    differs), matching the oracle."""
     monkeypatch.setenv("CGX_COOP_TAGR", tagr)
     rp, cl, vl = oracle.poisson(2, 128, 128, 1)
     n = len(rp) - 1

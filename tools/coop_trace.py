@@ -43,8 +43,8 @@ def main():
                 check(L.cgx_cg_destroy(cg))
                 continue
             check(L.cgx_cg_config(cg, 8, 0))  # 64 bodies per launch
-            R, G, T = C.c_int(), C.c_int(), C.c_int()
-            check(L.cgx_cg_coop_shape(cg, C.byref(R), C.byref(G), C.byref(T)))
+            R, NT, G, T = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+            check(L.cgx_cg_coop_shape(cg, C.byref(R), C.byref(NT), C.byref(G), C.byref(T)))
             check(L.cgx_cg_begin(cg, C.c_void_p(b.data_ptr()), C.c_void_p(x.data_ptr()), 0.0, 64))
             bodies, stopped = C.c_int64(), C.c_int()
             check(L.cgx_cg_run(cg, 64, C.byref(bodies), C.byref(stopped)))
