@@ -539,6 +539,8 @@ def coop_roofline(L, cg, avg, calls, bodies: int, iter_bytes: int) -> dict:
     is latency-bound (two grid-wide exchanges, one gather round trip); its
     vectors stay in the L2s and the Infinity Cache, so no HBM traffic is
     claimed (PMC FETCH_SIZE would count the exchanges' L2-bypassing loads)."""
+    from conjugategradient_amd._native import check
+
     R, NT, G, T = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     check(L.cgx_cg_coop_shape(cg, C.byref(R), C.byref(NT), C.byref(G), C.byref(T)))
     t_launch = avg[1] * 1e-3
