@@ -1698,7 +1698,11 @@ template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
       PV v;
       v.x = s0;
       v.y = s1;
+#ifdef CGX_AP_NT
+      __builtin_nontemporal_store(v, reinterpret_cast<PV *>(Ap + i));
+#else
       *reinterpret_cast<PV *>(Ap + i) = v;
+#endif
     } else {
       if (l0) Ap[i] = s0;
       if (l1) Ap[i + 1] = s1;

@@ -30,6 +30,9 @@ def matrix(q, name):
         return cga.Matrix.poisson(q, 3, 128, 128, 128)
     if name == "2d4096":
         return cga.Matrix.poisson(q, 2, 4096, 4096, 1)
+    if name.startswith("g2:") or name.startswith("g3:"):  # g3:NXxNYxNZ, g2:NXxNY
+        dims = [int(v) for v in name[3:].split("x")]
+        return cga.Matrix.poisson(q, int(name[1]), *dims)
     if name == "irr":
         from tests.util import irregular_spd
         rp, cl, vl = irregular_spd(1_585_478, mean_deg=3.83, seed=12345)
