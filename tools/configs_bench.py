@@ -57,8 +57,11 @@ def main():
     print("|---|---|---|---|---|---|---|---|---|")
     for name, ln in rows:
         r = ln.get("roofline") or {}
+        kern = (f"{r.get('kernel')}{r['template']} (whole body)" if r.get("template")
+                else f"{r.get('kernel')}<{ln['config']['spmv_variant']}>")
+        us = r.get("us_per_body") or r.get("avg_us")
         print(f"| {name} | {ln['iterations_per_s']:,} | {ln['value']:,} | {ln['iteration_frac']} | "
-              f"{r.get('kernel')}<{ln['config']['spmv_variant']}> | {r.get('avg_us')} | "
+              f"{kern} | {us} | "
               f"{r.get('frac')} | {r.get('traffic_ratio_to_compulsory')} | "
               f"{ln['csr_equivalent_GBs']:,} |", flush=True)
 
