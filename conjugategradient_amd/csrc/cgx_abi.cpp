@@ -774,6 +774,37 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
 int build_value_codes(cgx_csr *A);
 void free_sell(cgx_csr *A);
 
+// CSR-stream's 16-bit column deltas (variant bit kC16): built on demand;
+// false when some entry's delta from its row block's first row does not fit
+static void free_col16(cgx_csr *A) {
+  if (A->d_col16) (void)hipFree(A->d_col16);
+  A->d_col16 = nullptr;
+  A->dev.col16 = nullptr;
+}
+static bool build_col16(cgx_csr *A) {
+  if (A->dev.col16) return true;
+  if (A->dev.nnz < 2 || A->dev.nrb < 1 || !A->dev.rb || !A->dev.rbk) return false;
+  hipStream_t s = A->ctx->stream;
+  void *d = nullptr;
+  unsigned *bad = nullptr;
+  hipError_t e = hipMalloc(&d, (size_t)(A->dev.nnz + 2) * sizeof(short));
+  if (e == hipSuccess) e = hipMalloc((void **)&bad, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(unsigned), s);
+  if (e == hipSuccess) e = col16_build(A->dev, (short *)d, bad, s);
+  unsigned h = 1;
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, bad, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (bad) (void)hipFree(bad);
+  if (e != hipSuccess || h != 0) {
+    if (d) (void)hipFree(d);
+    (void)hipGetLastError();
+    return false;
+  }
+  A->d_col16 = d;
+  A->dev.col16 = (const short *)d;
+  return true;
+}
+
 // ===========================================================================
 // CSR
 // ===========================================================================
@@ -854,6 +885,7 @@ static void csr_free(cgx_csr *A) {
     if (A->d_rb) (void)hipFree(A->d_rb);
     if (A->d_ext) (void)hipFree(A->d_ext);
     free_sell(A);
+    free_col16(A);
     peer_destroy(A);
     dist_destroy_halo(A);
   }
@@ -1548,7 +1580,7 @@ extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
   else if (v & 2048)
     *bytes = es * A->sell_padded + 8 * A->sell_idx_words + desc;
   else
-    *bytes = (es + 4) * A->dev.nnz + 4 * (A->dev.n + 1);
+    *bytes = (es + ((v & kC16) ? 2 : 4)) * A->dev.nnz + 4 * (A->dev.n + 1);
   return CGX_OK;
 }
 
@@ -1582,7 +1614,7 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
 }
 
 static bool known_variant(int v) {
-  static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 264, 265, 266,
+  static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 133, 135, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
                            34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
                            821248, 821250, 1607680, 1607682, 1869824, 1869826,
@@ -1607,6 +1639,12 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
               "variant %d needs 4-bit value codes (at most 15 distinct values)", variant);
   CGX_REQUIRE(!(variant & kVT) || A->dev.sl_t, CGX_EUNSUPPORTED,
               "variant %d needs value-code templates, which this matrix does not have", variant);
+  if ((variant & kC16) && !(variant & 8192)) {
+    DeviceGuard g(A->ctx->device);
+    CGX_REQUIRE(build_col16(A), CGX_EUNSUPPORTED,
+                "variant %d needs 16-bit column deltas: a column of this matrix lies more than "
+                "32767 rows from its row block's first row", variant);
+  }
   // the bit mask is not enough: check the form the request resolves to on
   // this matrix has a kernel (e.g. 2138112, plane march without the pipe
   // bits, has none)
@@ -1660,6 +1698,8 @@ int autotune_spmv(cgx_csr *A) {
   // quad loads (265): the G3 stand-in's SpMV runs 23.6 / 23.8 us in them
   // against 25.3 in the pipelined 13 (profiles/r02_irr_variants.log)
   std::vector<int> cands = big ? std::vector<int>{15} : std::vector<int>{13, 15, 5, 265};
+  // and the paired loop on 16-bit column deltas (10 B per entry) where they fit
+  if (!big && build_col16(A)) cands.push_back(133);
   if (A->dev.sl) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
@@ -1772,6 +1812,7 @@ int autotune_spmv(cgx_csr *A) {
   CGX_HIP(e);
   A->dev.variant = best_v;
   if (!(best_v & (2048 | 8192))) free_sell(A);
+  if (!(best_v & kC16) || (best_v & 8192)) free_col16(A);
   return CGX_OK;
 }
 

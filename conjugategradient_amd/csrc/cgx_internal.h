@@ -99,6 +99,9 @@ constexpr int kVc4Max = 15;  // 4-bit codes: 15 values, 0xf empty
 // template copy of the slice table (CsrDev::sl_t) carries t + 1 in the high
 // half of its width (widths are at most 64).
 constexpr int kVT = 8388608;
+// CSR-stream with 16-bit column deltas (bit 128 on the paired loop: 133 =
+// 5 | 128): 10 bytes per entry instead of 12
+constexpr int kC16 = 128;
 constexpr int kVtMax = 8;
 constexpr int kVtWidthMask = 0xffff;
 
@@ -154,6 +157,10 @@ struct CsrDev {
   const SellSlice *sl_t = nullptr;
   const void *vct = nullptr;
   int nvt = 0;
+  // CSR-stream with 16-bit column deltas (variant bit kC16): entry k of row
+  // block b stores col[k] - rb[b] (every such delta fits int16; null when
+  // one does not or the copy was not built)
+  const short *col16 = nullptr;
 };
 
 // The templates apply to the pipelined 4-bit value-code walks (bits 524288,
@@ -295,6 +302,9 @@ constexpr int kCoopTraceWords = kCoopMaxG * 8 * 8;  // workgroups x bodies 8-15 
 hipError_t vc_hash(const CsrDev &A, unsigned long long *hash, hipStream_t s);
 hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, SellSlice *sl_t,
                     unsigned *count, hipStream_t s);
+// the 16-bit column deltas of A's row blocks into col16 (nnz + 2 entries);
+// *bad counts the entries whose delta does not fit
+hipError_t col16_build(const CsrDev &A, short *col16, unsigned *bad, hipStream_t s);
 
 // the SpMV variant a launch on A uses (dtype: CGX_F64 / CGX_F32)
 int launch_variant(const CsrDev &A, int dtype);

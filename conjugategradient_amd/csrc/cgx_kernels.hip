@@ -305,6 +305,7 @@ struct CsrArgs {
   int wg0;
   // value-code templates (kVT; sl is then the template slice table)
   const unsigned long long *vct;
+  const short *__restrict__ col16;  // 16-bit column deltas (kC16)
   int nvt;
 };
 
@@ -497,7 +498,18 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
           for (int u = 0; u < U; ++u) {
             const int j = min(t + u * kBlock, npairs - 1);
             v[u] = ldg<NT>(v2 + j);
-            c[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, k0 + cnt);
+            if constexpr ((V & kC16) != 0) {
+              // 16-bit deltas from the block's first row; a pair's element
+              // outside the block (the one before k0 when k0 is odd, those
+              // past its end) is relative to another block: it takes r0
+              typedef short S2 __attribute__((ext_vector_type(2)));
+              const S2 h = ldg<NT>(reinterpret_cast<const S2 *>(A.col16 + ka) + j);
+              const int e0 = ka + 2 * j;
+              c[u].x = (e0 >= k0 && e0 < k0 + cnt) ? r0 + (int)h.x : r0;
+              c[u].y = (e0 + 1 >= k0 && e0 + 1 < k0 + cnt) ? r0 + (int)h.y : r0;
+            } else {
+              c[u] = tail_cols(ldg<NT>(c2 + j), ka + 2 * j, k0 + cnt);
+            }
           }
           T g0[U], g1[U];
 #pragma unroll
@@ -2647,6 +2659,7 @@ inline CsrArgs args(const CsrDev &A) {
     a.vct = static_cast<const unsigned long long *>(A.vct);
     a.nvt = A.nvt;
   }
+  a.col16 = A.col16;
   return a;
 }
 
@@ -3003,9 +3016,11 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   // bits 16/32: timing ablations, only reachable through cgx_tune_spmv; the
   // retired half-tile (64), three-stage (128) and wave-tile (512) bits drop
   // (a schedule built for smaller tiles fits the full-tile kernels)
+  const bool c16 = (v & kC16) && A.col16 && (v & 4) && !(v & (8 | 256));
   v &= 1023 & ~(64 | 128 | 512);
   if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2)
     return 0;  // plain loads, no pipelining (any schedule with <= 2042-entry blocks)
+  if (c16) return v | kC16;  // 132..135: paired loop, 16-bit column deltas
   if ((v & 256) && (((uintptr_t)A.val % (4 * sizeof(T))) || ((uintptr_t)A.col % 16) ||
                     A.nnz < 4))
     v &= ~256;  // quads need 4-entry alignment
@@ -3049,6 +3064,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 265: CGX_LAUNCH_V(KERNEL, 265, __VA_ARGS__);          \
     case 266: CGX_LAUNCH_V(KERNEL, 266, __VA_ARGS__);          \
     case 267: CGX_LAUNCH_V(KERNEL, 267, __VA_ARGS__);          \
+    case 133: CGX_LAUNCH_V(KERNEL, 133, __VA_ARGS__);          \
+    case 135: CGX_LAUNCH_V(KERNEL, 135, __VA_ARGS__);          \
     case 2048: CGX_LAUNCH_V(KERNEL, 2048, __VA_ARGS__);        \
     case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);        \
     case 2056: CGX_LAUNCH_V(KERNEL, 2056, __VA_ARGS__);        \
@@ -3092,6 +3109,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 // turns the cap off (A/B).
 #define CGX_SPMV_LIST(X)                                                                    \
   X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(264) X(265) X(266)      \
+  X(133) X(135)                                                                             \
   X(267) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578)  \
   X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
   X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122) X(40978)     \
@@ -3252,7 +3270,7 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
 // mode 2 (k_spmv_fused): mode 4's forms, plain CSR-stream and the
 // dictionary SELL forms small matrices take
 #define CGX_FUSED_LIST(X)                                                                \
-  CGX_FD_LIST(X) X(0) X(5) X(265) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(24576) \
+  CGX_FD_LIST(X) X(0) X(5) X(133) X(265) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(24576) \
   X(24578)
 
 template <typename T> static const void *spmv_fd_kernel(int v) {
@@ -3551,6 +3569,34 @@ hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, Sel
   const int g = (int)((A.nsl + 3) / 4);
   hipLaunchKernelGGL(k_vc_match, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
                      (const unsigned long long *)A.svc4, tmpl, nt, sl_t, count);
+  return hipGetLastError();
+}
+
+// 16-bit column deltas (kC16): one workgroup per row block (grid-stride)
+__global__ __launch_bounds__(kBlock) void k_col16(const int *__restrict__ rb,
+                                                   const int *__restrict__ rbk,
+                                                   const int *__restrict__ col, int nrb,
+                                                   short *__restrict__ col16, unsigned *bad) {
+  unsigned nbad = 0;
+  for (int b = blockIdx.x; b < nrb; b += gridDim.x) {
+    const int r0 = rb[b];
+    for (int k = rbk[b] + threadIdx.x; k < rbk[b + 1]; k += kBlock) {
+      const int d = col[k] - r0;
+      const bool fits = d >= -32768 && d <= 32767;
+      col16[k] = fits ? (short)d : (short)0;
+      nbad += fits ? 0u : 1u;
+    }
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+hipError_t col16_build(const CsrDev &A, short *col16, unsigned *bad, hipStream_t s) {
+  if (A.nrb < 1) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(col16, 0, (size_t)(A.nnz + 2) * sizeof(short), s);
+  if (e != hipSuccess) return e;
+  const int grid = A.nrb < kMaxGrid ? A.nrb : kMaxGrid;
+  hipLaunchKernelGGL(k_col16, dim3(grid), dim3(kBlock), 0, s, A.rb, A.rbk, A.col, A.nrb, col16,
+                     bad);
   return hipGetLastError();
 }
 

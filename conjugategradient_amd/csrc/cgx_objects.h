@@ -160,6 +160,7 @@ struct cgx_csr {
   void *d_sell_vc4 = nullptr;                          // 4-bit value codes
   void *d_sell_sl_t = nullptr, *d_vct = nullptr;       // value-code templates (kVT)
   int64_t vt_slices = 0;                               // slices that read a template
+  void *d_col16 = nullptr;  // CSR-stream 16-bit column deltas (cgx::CsrDev::col16)
   // partitioned SELL matrix: slices without ghost columns, then those with
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;

@@ -77,7 +77,7 @@ def test_g3_standin_spmv_bitexact(queue, oracle, g3):
     assert not (_variant(m) & 32768)  # too many distinct values for codes
     x = np.random.default_rng(3).standard_normal(G3_N)
     want = oracle.spmv(rp, cl, vl, x)
-    for v in (0, 5, 13, 15, 265):  # autotune's pick, then the CSR forms it tries
+    for v in (0, 5, 13, 15, 265, 133, 135):  # autotune's pick, the CSR forms it tries
         if v:
             check(lib().cgx_csr_set_variant(m.schedule(), v))
         y = cga.Vector(queue, G3_N)
