@@ -186,6 +186,14 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
     const int gi = !split ? 0
                    : merged ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
                             : Launch<T>::slice_grid(A->dev, A->split_ni);
+    // the boundary slices wait for the neighbours' pushes themselves and read
+    // the ghosts from the landing buffer (k_spmv_dot_bnd): no k_peer_wait
+    // launch, no copy into p's ghost tail; $CGX_PEER_WAIT_FOLD=0 keeps them
+    static const bool fold_on = [] {
+      const char *e = std::getenv("CGX_PEER_WAIT_FOLD");
+      return !e || std::atoi(e) != 0;
+    }();
+    const bool fold = split && A->split_nb > 0 && fold_on && Launch<T>::bnd_supported(A->dev);
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = hipSuccess;
            if (merged)
@@ -194,6 +202,10 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
+           if (e == hipSuccess && fold)
+             return Launch<T>::spmv_dot_slices_bnd(A->dev, A->d_split + A->split_ni,
+                                                   A->split_nb, gi, p, Ap, st, slot, ws, s, rev,
+                                                   A->peer.dev);
            if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
            if (e == hipSuccess)
              e = split ? Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,

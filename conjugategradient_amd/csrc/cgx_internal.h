@@ -220,6 +220,13 @@ template <typename T> struct Launch {
                                          int part_off, const T *p, T *Ap, CgScalars<T> *st,
                                          int slot, RedWs<T> *ws, hipStream_t s, int rev,
                                          const PeerDev &P, int wg0);
+  // the boundary launch with the peer transport's halo wait folded in: ghost
+  // values read from the landing buffer (k_spmv_dot_bnd)
+  static bool bnd_supported(const CsrDev &A);
+  static hipError_t spmv_dot_slices_bnd(const CsrDev &A, const int *list, int count,
+                                        int part_off, const T *p, T *Ap, CgScalars<T> *st,
+                                        int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                        const PeerDev &P);
   static int update_parts(int64_t n);
   // *dst = sum of part[0..np) (one workgroup; partitioned runs, before RCCL)
   static hipError_t finalize(const T *part, int np, T *dst, hipStream_t s);

@@ -417,6 +417,36 @@ template <typename T> struct GatherX {
     return ((const __attribute__((address_space(4))) T *)x)[i];
   }
 };
+// The boundary slices of a partitioned matrix with the peer transport's wait
+// folded in (k_spmv_dot_bnd): x below n is this rank's p, from n on the
+// ghost values are read where the neighbours pushed them, the landing buffer
+// (uncached memory, its entry k is ghost n + k), instead of from p's ghost
+// tail after a copy. Scalar reads of the landing buffer go through vector
+// loads (no scalar-cache copy of memory other GPUs rewrite every body).
+template <typename T> struct GatherXL {
+  const T *__restrict__ x;
+  const T *__restrict__ land;
+  int n;
+  __device__ __forceinline__ T operator()(int c) const { return c < n ? x[c] : land[c - n]; }
+  __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
+    using U = typename PairU<T>::V;
+    if (c + 1 < n) return *reinterpret_cast<const U *>(x + c);
+    if (c >= n) return *reinterpret_cast<const U *>(land + (c - n));
+    U r;  // the pair across the boundary: p[n - 1], ghost n
+    r.x = x[c];
+    r.y = land[0];
+    return r;
+  }
+  __device__ __forceinline__ typename PairU<T>::V pair_b(unsigned b) const {
+    return pair((int)(b / (unsigned)sizeof(T)));
+  }
+  __device__ __forceinline__ T at_s(int i) const {
+    if (i < n) return ((const __attribute__((address_space(4))) T *)x)[i];
+    return __hip_atomic_load(const_cast<T *>(land + (i - n)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+};
+
 // NTP: p_{k-1} read non-temporally (the plane march reads each of its lines
 // once as a center; mode 4 reads it again only in the slot-3 x flush)
 template <typename T, bool NTP = false> struct GatherP {
@@ -1955,6 +1985,45 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
 }
 
+// The boundary slices with the peer transport's wait folded in (round 3;
+// DESIGN.md §9): every workgroup's first wave polls the push flags of every
+// rank that sends here for this body's tag (k_peer_wait's poll, bounded),
+// then the workgroup runs its slices gathering ghosts from the landing
+// buffer (GatherXL). It waits only on other GPUs' pushes, which were raised
+// by their interior launches and depend on nothing in this launch, so the
+// protocol needs no workgroup of this launch to be resident or dispatched
+// before another. One launch per body less than push / wait / boundary.
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_bnd(
+    CsrArgs A, const T *__restrict__ val, const T *__restrict__ p, T *__restrict__ Ap,
+    CgScalars<T> *st, int slot, RedWs<T> *ws, PeerDev P) {
+  if (peerdev::skip_body(st, slot, P.state)) return;
+  __shared__ int ok_s;
+  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
+  if (threadIdx.x < 64) {
+    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
+    bool ok = true;
+    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
+      ok = ok && peerdev::spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
+                                  P.spin_ticks);
+    ok = __all(ok);
+    if (threadIdx.x == 0) ok_s = ok;
+  }
+  __syncthreads();
+  if (!ok_s) {
+    if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, as k_peer_wait
+  __shared__ LdsOf<T, V> sm;
+  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
+  spmv_any<T, V>(A, val, GatherXL<T>{p, reinterpret_cast<const T *>(P.land_local), (int)A.n}, e,
+                 sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
 // Fused deferred-x iteration (mode 4), kernel 1 of 2 for body k in slot s
 // (cgx_abi.cpp enqueue_iter_fdefer): p_k into P[s] from r and P[s-1] (EpiFD),
 // helper = A p_k, this workgroup's p.Ap partial. beta_{k-1} = r.r / rxr from
@@ -3350,6 +3419,38 @@ template <typename T> static const void *spmv_push_kernel(int v) {
 #undef CGX_KPU
     default: return nullptr;
   }
+}
+
+template <typename T> static const void *spmv_bnd_kernel(int v) {
+  switch (v) {
+#define CGX_KBN(VV) \
+  case VV: return reinterpret_cast<const void *>(&k_spmv_dot_bnd<T, VV>);
+    CGX_PUSH_LIST(CGX_KBN)
+#undef CGX_KBN
+    default: return nullptr;
+  }
+}
+template <typename T> bool Launch<T>::bnd_supported(const CsrDev &A) {
+  return spmv_bnd_kernel<T>(spmv_variant<T>(A) & ~2097152) != nullptr;
+}
+template <typename T>
+hipError_t Launch<T>::spmv_dot_slices_bnd(const CsrDev &A, const int *list, int count,
+                                          int part_off, const T *p, T *Ap, CgScalars<T> *st,
+                                          int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                          const PeerDev &P) {
+  const int v = spmv_variant<T>(A) & ~2097152;
+  const void *k = spmv_bnd_kernel<T>(v);
+  if (!k || count < 1) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.sorder = list;
+  a.nsl = count;
+  a.part_off = part_off;
+  a.rev = rev;
+  const T *val = (const T *)A.val;
+  PeerDev pd = P;
+  void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
+                   (void *)&ws, (void *)&pd};
+  return hipLaunchKernel(k, dim3(slice_grid(A, count)), dim3(kBlock), kargs, 0, s);
 }
 
 template <typename T> bool Launch<T>::push_supported(const CsrDev &A) {

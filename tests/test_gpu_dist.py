@@ -32,12 +32,13 @@ def _port():
     return p
 
 
-def _run(nproc, transport, grid, mode=0, extra=(), timeout=300):
+def _run(nproc, transport, grid, mode=0, extra=(), timeout=300, env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "dist_check.py"), "--transport", transport,
            "--grid", str(grid), "--mode", str(mode), *extra]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
+                       env=None if env is None else {**os.environ, **env})
     assert p.returncode == 0, p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     return json.loads(line)
@@ -81,6 +82,17 @@ def test_async_host_halo_matches_synchronous(nproc, grid, mode):
     assert rs["async_exchanges"] == [0] * nproc
     assert ra["bodies"] == rs["bodies"]
     assert ra["x_sha"] == rs["x_sha"]
+
+
+@pytest.mark.parametrize("nproc,mode", [(3, 3), (2, 1)])
+def test_peer_boundary_without_the_folded_wait(nproc, mode):
+    """The boundary slices wait for the pushes themselves and read the ghosts
+    from the landing buffer (k_spmv_dot_bnd, the default above); with
+    $CGX_PEER_WAIT_FOLD=0 the separate k_peer_wait copies them into p's
+    ghost tail first. Both match the oracle."""
+    r = _run(nproc, "host-peer", 20, mode, env={"CGX_PEER_WAIT_FOLD": "0"})
+    assert r["ok"], r
+    assert r["peer"] == [1] * nproc
 
 
 def test_partitioned_slab_of_the_8gpu_config():
