@@ -2295,6 +2295,11 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
               "$CGX_PEER_TIMEOUT_S is too short); the solve was stopped");
     return CGX_ENCCL;
   }
+  if (last_stopped == 4) {
+    set_error("mode 5: a grid-wide exchange of the persistent body timed out (a workgroup of "
+              "the launch was not resident); the solve was stopped, x is not updated");
+    return CGX_EHIP;
+  }
   if ((rc = flush_pending_x(cg))) return rc;
   CGX_HIP(hipStreamSynchronize(s));
   if (cg->timing) {

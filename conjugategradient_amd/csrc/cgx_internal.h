@@ -35,7 +35,8 @@ template <typename T> struct CgScalars {
   long long bodies;  // loop bodies executed (the reference's counter + 1)
   long long cap;     // max bodies: N+1 (CG.hpp:436) or a caller cap
   int stopped;       // 0 running, 1 stop rule (tol / NaN), 2 cap reached,
-                     // 3 peer transport fault (a spin timed out)
+                     // 3 peer transport fault (a spin timed out), 4 a mode-5
+                     // grid-wide exchange timed out
   int pad_i;
   // deferred x update (mode 3, cgx_abi.cpp enqueue_iter_defer): alpha of the
   // body in slot s, set by its update_r; ran[s]: the body ran and its x
