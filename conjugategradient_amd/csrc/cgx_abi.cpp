@@ -399,7 +399,8 @@ int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
                    (double *)cg->x, (double *)cg->r, (double *)cg->p, (double *)cg->p2,
                    (unsigned long long *)cg->coop_rg, (CgScalars<double> *)cg->st, slot, m,
                    (CoopWs *)cg->coop_ws, cg->coop_ticks,
-                   (unsigned long long *)cg->coop_trace, cg->coop_nap, cg->ctx->stream);
+                   (unsigned long long *)cg->coop_trace, cg->coop_nap, cg->coop_stall,
+                   cg->ctx->stream);
   });
 }
 
@@ -2025,6 +2026,8 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     if (const char *e = std::getenv("CGX_COOP_NT")) cg->coop_nt = std::atoi(e);
     if (const char *e = std::getenv("CGX_COOP_NAP")) cg->coop_nap = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
+    cg->coop_stall = -1;
+    if (const char *e = std::getenv("CGX_COOP_INJECT_STALL")) cg->coop_stall = std::atoi(e);
   }
   if (mode == 5) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
@@ -2069,6 +2072,8 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
         clk_khz <= 0)
       clk_khz = 100000;  // 100 MHz on gfx9
     cg->coop_ticks = (long long)clk_khz * 1000 * 2;  // 2 s: a resident grid never waits so long
+    if (const char *e = std::getenv("CGX_COOP_TIMEOUT_MS"))
+      cg->coop_ticks = (long long)clk_khz * std::max(1, std::atoi(e));
   }
   cg->coop = c;
   if (c) cg->coop_r = coop_r;

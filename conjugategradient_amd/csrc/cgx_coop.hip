@@ -262,7 +262,7 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
     int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, double *__restrict__ x, double *r, double *p0, double *p1,
     CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks,
-    unsigned long long *trace, int nap) {
+    unsigned long long *trace, int nap, int stall) {
   CGX_COOP_PROLOGUE
   double beta = 0.0;
   for (int i = 0; i < m; ++i) {
@@ -312,7 +312,9 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
     drain();  // this wave's p stores are out before the workgroup publishes
     part = block_sum<NT>(part, red[0]);
     CGX_COOP_TR(2)
-    publish(cw->ga, part, tag);
+    // fault injection (tests): workgroup 0 withholds body `stall`'s p.Ap
+    // partial, so every other workgroup's bounded spin gives up
+    if (!(i == stall && blockIdx.x == 0)) publish(cw->ga, part, tag);
     if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
     CGX_COOP_TR(3)
     const double pAp = res;
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
     int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
     const double *__restrict__ val, double *__restrict__ x, double *r, double *p0,
     unsigned long long *pg, unsigned long long *rg, CgScalars<double> *st, int slot0, int m,
-    CoopWs *cw, long long ticks, unsigned long long *trace, int nap) {
+    CoopWs *cw, long long ticks, unsigned long long *trace, int nap, int stall) {
   CGX_COOP_PROLOGUE
   double gp[R][kCoopK], gr[R][kCoopK];  // this body's gathered p_{k-1}[j] (body 0: p_k) and r_k[j]
 #pragma unroll
@@ -416,7 +418,9 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
     for (int u = 0; u < R; ++u) part += pv[u] * q[u];
     part = block_sum<NT>(part, red[0]);
     CGX_COOP_TR(2)
-    publish(cw->ga, part, tag);
+    // fault injection (tests): workgroup 0 withholds body `stall`'s p.Ap
+    // partial, so every other workgroup's bounded spin gives up
+    if (!(i == stall && blockIdx.x == 0)) publish(cw->ga, part, tag);
     if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
     CGX_COOP_TR(3)
     const double pAp = res;
@@ -500,7 +504,8 @@ int coop_rows_per_thread(int64_t n, int want, int nt) {
 hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
                    unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
-                   long long ticks, unsigned long long *trace, int nap, hipStream_t s) {
+                   long long ticks, unsigned long long *trace, int nap, int stall,
+                   hipStream_t s) {
   const int G = (int)((n + (int64_t)NT * R - 1) / ((int64_t)NT * R));
   if (G < 1 || G > kCoopMaxG || m < 1 || (tagged && !g)) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
@@ -509,10 +514,10 @@ hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, con
   unsigned long long *pg = g, *rg = g ? g + 4 * n : nullptr;
 #define CGX_COOP_WT(RR, TT)                                                                 \
   k_cg_coop_wt<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
-                                        ticks, trace, nap)
+                                        ticks, trace, nap, stall)
 #define CGX_COOP_TG(RR, TT)                                                                 \
   k_cg_coop_tg<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, pg, rg, st, slot0, m, \
-                                        cw, ticks, trace, nap)
+                                        cw, ticks, trace, nap, stall)
   const int key = (NT == 1024 ? 100 : NT == 512 ? 50 : 0) + R * 2 + (tagged ? 1 : 0);
   switch (key) {
     case 2: CGX_COOP_WT(1, 256); break;

@@ -301,7 +301,8 @@ int coop_rows_per_thread(int64_t n, int want, int nt);
 hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
                    unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
-                   long long ticks, unsigned long long *trace, int nap, hipStream_t s);
+                   long long ticks, unsigned long long *trace, int nap, int stall,
+                   hipStream_t s);
 constexpr int kCoopTraceWords = kCoopMaxG * 8 * 8;  // workgroups x bodies 8-15 x phases
 
 // value-code templates (cgx_abi.cpp build_value_templates): per slice the

@@ -186,6 +186,8 @@ struct cgx_cg {
   int coop_r = 0;       // its rows per thread
   int coop_nt = 1024;   // threads per workgroup ($CGX_COOP_NT: 256, 512 or 1024)
   int coop_nap = 1;     // s_sleep(1)s per exchange poll ($CGX_COOP_NAP)
+  int coop_stall = -1;  // tests: a launch's body whose p.Ap partial workgroup 0
+                        // withholds ($CGX_COOP_INJECT_STALL; -1 none)
   void *coop_ws = nullptr;  // cgx::CoopWs
   void *coop_rg = nullptr;  // tagged p and r granules (6 n words; $CGX_COOP_TAGR=1)
   bool coop_tagr = false;

@@ -143,3 +143,24 @@ def test_mode5_r_handoff_forms(queue, oracle, monkeypatch, tagr):
     assert r5 == r5b
     _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 60, 8)
     assert rel(x5, xr) <= 1e-10
+
+
+def test_mode5_stalled_exchange_times_out_and_recovers(queue, oracle, monkeypatch):
+    """Every spin of the persistent body is bounded: with workgroup 0
+    withholding one body's p.Ap partial (fault injection), the others give
+    up after $CGX_COOP_TIMEOUT_MS and raise the shared flag, the launch ends,
+    cgx_cg_run reports it (stopped = 4), and the device and a new solver
+    work normally afterwards."""
+    rp, cl, vl = oracle.poisson(2, 64, 64, 1)
+    n = len(rp) - 1
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    monkeypatch.setenv("CGX_COOP_INJECT_STALL", "3")
+    monkeypatch.setenv("CGX_COOP_TIMEOUT_MS", "50")
+    with pytest.raises(Exception, match="mode 5"):
+        _solve(queue, m, b, 5, 0.0, max_iter=20)
+    monkeypatch.delenv("CGX_COOP_INJECT_STALL")
+    monkeypatch.delenv("CGX_COOP_TIMEOUT_MS")
+    x5, it5, _ = _solve(queue, m, b, 5, 0.0, max_iter=20)
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 20, 8)
+    assert it5 == 20 and rel(x5, xr) <= 1e-10
