@@ -361,6 +361,17 @@ constexpr bool kStreamNt = false;
 #else
 constexpr bool kStreamNt = true;
 #endif
+// ... but only for vectors too large for the working set to stay in the
+// Infinity Cache: with vectors of <= 32 MB (the 256^3/8 slab's 16.8 MB, the
+// G3 stand-in's 12.7 MB) every vector of the iteration is re-read from it,
+// and plain loads and stores ran the slab bodies 2-3% faster
+// (profiles/r03_slab_nt.log)
+#ifndef CGX_NT_VEC_BYTES
+#define CGX_NT_VEC_BYTES (int64_t(32) << 20)
+#endif
+template <typename T> __device__ __forceinline__ bool stream_nt(int64_t n) {
+  return kStreamNt && n * (int64_t)sizeof(T) > CGX_NT_VEC_BYTES;
+}
 // HIP vector types (double2, float2 of element T): non-temporal through the
 // native vector of two T
 template <bool NT, typename T, typename P> __device__ __forceinline__ P ldv(const P *p) {
@@ -2178,7 +2189,7 @@ template <typename T> __device__ __forceinline__ void peer_fault(CgScalars<T> *s
   }
 }
 
-template <typename T, bool FUSED, bool PEER>
+template <typename T, bool FUSED, bool PEER, bool SNT>
 // rin == r: in place (modes 1, 2); else r ping-pongs between two buffers.
 __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
                                               const T *__restrict__ Ap, CgScalars<T> *st,
@@ -2222,7 +2233,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   for (int u = 0; u < 4; ++u) {  // clamped (r and Ap have a slack element): no branch
     const int64_t j = E(min(i + u * stride, n2 > 0 ? n2 - 1 : 0));
     rv[u] = ri2[j];
-    av[u] = ldv<kStreamNt, T>(a2 + j);  // Ap is dead after this kernel
+    av[u] = ldv<SNT, T>(a2 + j);  // Ap is dead after this kernel
   }
 #if CGX_LATE_ACTIVE
   if (!act) {
@@ -2271,7 +2282,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         rv[u] = ri2[E(i + u * stride)];
-        av[u] = ldv<kStreamNt, T>(a2 + E(i + u * stride));
+        av[u] = ldv<SNT, T>(a2 + E(i + u * stride));
       }
     }
 #pragma unroll
@@ -2326,7 +2337,11 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
                                                      CgScalars<T> *st, int slot,
                                                      RedWs<T> *ws, int np_pap, int rev,
                                                      int rule) {
-  update_r_body<T, FUSED, false>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule, nullptr);
+  if (stream_nt<T>(n))
+    update_r_body<T, FUSED, false, true>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule, nullptr);
+  else
+    update_r_body<T, FUSED, false, false>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule,
+                                          nullptr);
 }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
@@ -2334,7 +2349,10 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
                                                           CgScalars<T> *st, int slot,
                                                           RedWs<T> *ws, int np_pap, int rev,
                                                           PeerDev P) {
-  update_r_body<T, false, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
+  if (stream_nt<T>(n))
+    update_r_body<T, false, true, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
+  else
+    update_r_body<T, false, true, false>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
 }
 
 // x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
@@ -2788,7 +2806,7 @@ template <typename T> int Launch<T>::grid_elems(int64_t n, int cap) {
 // 8 N + 8 N (x) + 24 N (p0..p2) bytes once instead of 16 N four times.
 // In slot 3, pn is P0 (p_{k+1} replaces p_{k-3}): every element's flush
 // operands are loaded before its stores, and pn / P0 carry no __restrict__.
-template <typename T, bool FLUSH, bool PEER>
+template <typename T, bool FLUSH, bool PEER, bool SNT>
 __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x, const T *p,
                                                     T *pn, const T *P0, const T *P1,
                                                     const T *P2, const T *__restrict__ r,
@@ -2861,13 +2879,13 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
     // to p_{k+1}, which the next SpMV reads first (+2.9% per iteration at
     // 256^3: SpMV 90.3 against 93.2 us, this kernel 88.4 against 91.3;
     // profiles/r02_pupd_nt.log)
-    const V pv = ldv<kStreamNt, T>(p2 + i);
-    const V rv = ldv<kStreamNt, T>(rv2 + i);
+    const V pv = ldv<SNT, T>(p2 + i);
+    const V rv = ldv<SNT, T>(rv2 + i);
     V q[3], xv;
     if constexpr (FLUSH) {  // x and the old p buffers: not read again soon
-      xv = ldv<kStreamNt, T>(x2 + i);
+      xv = ldv<SNT, T>(x2 + i);
 #pragma unroll
-      for (int t = 0; t < 3; ++t) q[t] = ldv<kStreamNt, T>(Q[t] + i);  // before pn (= P0) is written
+      for (int t = 0; t < 3; ++t) q[t] = ldv<SNT, T>(Q[t] + i);  // before pn (= P0) is written
     }
     V o;
     o.x = rv.x + beta * pv.x;
@@ -2884,7 +2902,7 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
         xv.x = xv.x + a[3] * pv.x;
         xv.y = xv.y + a[3] * pv.y;
       }
-      stv<kStreamNt, T>(x2 + i, xv);
+      stv<SNT, T>(x2 + i, xv);
     }
     pn2[i] = o;
   };
@@ -2935,16 +2953,24 @@ __global__ __launch_bounds__(kBlock) void k_update_p_defer(int64_t n, T *__restr
                                                            const T *__restrict__ r,
                                                            CgScalars<T> *st, int slot,
                                                            RedWs<T> *ws, int np_rr, int rev) {
-  update_p_defer_body<T, FLUSH, false>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr, rev,
-                                       nullptr);
+  if (stream_nt<T>(n))
+    update_p_defer_body<T, FLUSH, false, true>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr,
+                                               rev, nullptr);
+  else
+    update_p_defer_body<T, FLUSH, false, false>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr,
+                                                rev, nullptr);
 }
 template <typename T, bool FLUSH>
 __global__ __launch_bounds__(kBlock) void k_update_p_defer_peer(
     int64_t n, T *__restrict__ x, const T *p, T *pn, const T *P0, const T *P1, const T *P2,
     const T *__restrict__ r, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr, int rev,
     PeerDev PD) {
-  update_p_defer_body<T, FLUSH, true>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr, rev,
-                                      &PD);
+  if (stream_nt<T>(n))
+    update_p_defer_body<T, FLUSH, true, true>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr,
+                                              rev, &PD);
+  else
+    update_p_defer_body<T, FLUSH, true, false>(n, x, p, pn, P0, P1, P2, r, st, slot, ws, np_rr,
+                                               rev, &PD);
 }
 
 // End of a run in mode 3: apply the bodies of the current group that ran and
@@ -3006,11 +3032,12 @@ __global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict
   V *x2 = reinterpret_cast<V *>(x);
   const V *Q[4] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
                    reinterpret_cast<const V *>(P2), reinterpret_cast<const V *>(P3)};
-  auto body = [&](int64_t i) {
-    V xv = ldv<kStreamNt, T>(x2 + i);
+  auto body = [&](int64_t i, auto sntc) {
+    constexpr bool S = decltype(sntc)::value;
+    V xv = ldv<S, T>(x2 + i);
     V q[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) q[t] = ldv<kStreamNt, T>(Q[t] + i);
+    for (int t = 0; t < 4; ++t) q[t] = ldv<S, T>(Q[t] + i);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (use[t]) {
@@ -3018,15 +3045,21 @@ __global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict
         xv.y = xv.y + a[t] * q[t].y;
       }
     }
-    stv<kStreamNt, T>(x2 + i, xv);
+    stv<S, T>(x2 + i, xv);
   };
   auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  for (; i + stride < n2; i += 2 * stride) {
-    body(E(i));
-    body(E(i + stride));
-  }
-  for (; i < n2; i += stride) body(E(i));
+  auto loop = [&](auto sntc) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + stride < n2; i += 2 * stride) {
+      body(E(i), sntc);
+      body(E(i + stride), sntc);
+    }
+    for (; i < n2; i += stride) body(E(i), sntc);
+  };
+  if (stream_nt<T>(n))
+    loop(std::true_type{});
+  else
+    loop(std::false_type{});
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     T xv = x[n - 1];
     const T *Ps[4] = {P0, P1, P2, P3};
