@@ -495,7 +495,8 @@ int coop_rows_per_thread(int64_t n, int want, int nt) {
   if (nt != 256 && nt != 512 && nt != 1024) return 0;
   for (int R : opts) {
     if (want > 0 && R != want) continue;
-    if (nt > 256 && R != 1) continue;
+    if (nt == 1024 && R != 1) continue;  // 128 VGPRs at 16 waves per CU
+    if (nt == 512 && R > 2) continue;    // <4, 512> spills
     if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= kCoopMaxG) return R;
   }
   return 0;
@@ -528,6 +529,7 @@ hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, con
     case 9: CGX_COOP_TG(4, 256); break;
     case 52: CGX_COOP_WT(1, 512); break;
     case 53: CGX_COOP_TG(1, 512); break;
+    case 54: CGX_COOP_WT(2, 512); break;
     case 102: CGX_COOP_WT(1, 1024); break;
     case 103: CGX_COOP_TG(1, 1024); break;
     default: return hipErrorInvalidValue;

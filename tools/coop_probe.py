@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shapes", default="", help="R:tagged:threads,... (mode 5 shapes to time)")
     a = ap.parse_args()
+    global VARIANTS
+    if a.shapes:
+        VARIANTS = [(0, None, None, None)] + [(5, *sh.split(":")) for sh in a.shapes.split(",")]
     L = lib()
     q = cga.Queue(0)
     import torch
