@@ -980,6 +980,7 @@ void free_sell(cgx_csr *A) {
   A->dev.sell_maxw = 0;
   A->dev.march_k = A->dev.march_a = A->dev.march_len = 0;
   A->dev.march_pat = -1;
+  A->dev.ymarch_k = A->dev.ymarch_a = 0;
   A->sell_padded = 0;
   A->sell_idx_words = 0;
   A->vc_chunks = 0;
@@ -1125,6 +1126,7 @@ static void plan_march(const std::vector<SellSlice> &sl, const std::vector<int> 
                        int64_t nx, size_t es, CsrDev &dev) {
   dev.march_k = dev.march_a = dev.march_len = 0;
   dev.march_pat = -1;
+  dev.ymarch_k = dev.ymarch_a = 0;
   if (const char *e = std::getenv("CGX_MARCH"))
     if (std::atoi(e) == 0) return;
   if (sl.empty() || (uint64_t)nx * es >= (uint64_t(1) << 32)) return;
@@ -1148,6 +1150,13 @@ static void plan_march(const std::vector<SellSlice> &sl, const std::vector<int> 
   dev.march_k = D / H;
   dev.march_a = a;
   dev.march_pat = base;
+  // the y-march of a 3-D pattern: lines of a = nx rows, a whole number of
+  // slices; the gathered offset is D
+  dev.ymarch_k = dev.ymarch_a = 0;
+  if (W == 7 && a % H == 0) {
+    dev.ymarch_k = a / H;
+    dev.ymarch_a = D;
+  }
   if (const char *e = std::getenv("CGX_MARCH_LEN")) dev.march_len = std::max(0, std::atoi(e));
 }
 
@@ -1636,8 +1645,8 @@ static bool known_variant(int v) {
     if (k == v) return true;
   // the resolved SELL-P forms cgx_csr_variant reports (e.g. 1875970) are
   // accepted back as requests
-  constexpr int sellp_bits =
-      8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 | 2097152 | kVT | 2;
+  constexpr int sellp_bits = 8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 |
+                             2097152 | kVT | kYM | 2;
   return (v & 8192) && !(v & ~sellp_bits);
 }
 
@@ -1723,10 +1732,14 @@ int autotune_spmv(cgx_csr *A) {
   // 1048576: one gather pair fewer per offset -1 / +1)
   for (int c4 : {0, 262144}) {
     if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
+    // (the y-march forms, kYM, measured 93-124 us against 72 for the
+    // templated consecutive walk at 256^3: reachable by request only,
+    // profiles/r03_ymarch_tune.log)
     for (int pipe : {0, 524288, 524288 | 1048576, 524288 | 1048576 | 2097152,
                      524288 | kVT, 524288 | 1048576 | kVT, 524288 | 1048576 | 2097152 | kVT}) {
       if (pipe && A->dev.sell_maxw > 8) continue;
       if ((pipe & 2097152) && A->dev.march_k < 1) continue;
+      if ((pipe & kYM) && (!c4 || A->dev.ymarch_k < 1)) continue;  // 4-bit forms only
       if ((pipe & kVT) && (!c4 || !A->dev.sl_t)) continue;
       if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
       cands.push_back(2050 | 32768 | c4 | pipe);
@@ -1776,6 +1789,13 @@ int autotune_spmv(cgx_csr *A) {
       if (e == hipSuccess) e = hipEventSynchronize(e1);
       if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
       if (e == hipSuccess) tbest[ci] = std::min(tbest[ci], tot);
+      if (e != hipSuccess) {
+        set_error("cgx_csr_create: SpMV autotune candidate %d (resolved %d) failed: %s", v,
+                  launch_variant(dv, A->dtype), hipGetErrorString(e));
+        for (void *p : {x, y, st})
+          if (p) (void)hipFree(p);
+        return CGX_EHIP;
+      }
     }
   }
   int best_v = 0;

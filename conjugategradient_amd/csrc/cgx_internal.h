@@ -100,6 +100,12 @@ constexpr int kVc4Max = 15;  // 4-bit codes: 15 values, 0xf empty
 // template copy of the slice table (CsrDev::sl_t) carries t + 1 in the high
 // half of its width (widths are at most 64).
 constexpr int kVT = 8388608;
+// y-march (variant bit kYM with the march bit 2097152): the
+// plane march's walk along y instead of z on a 3-D 7-point matrix: a wave
+// walks the slices of one half x-line through consecutive y lines (2 KB
+// steps), the +-nx neighbours come from registers and the +-nx*ny ones are
+// the gathers (CsrDev::ymarch_*)
+constexpr int kYM = 16777216;
 // CSR-stream with 16-bit column deltas (bit 128 on the paired loop: 133 =
 // 5 | 128): 10 bytes per entry instead of 12
 constexpr int kC16 = 128;
@@ -153,6 +159,9 @@ struct CsrDev {
   // SELL-P pattern is {-D, (-a,) -1, 0, 1, (a,) D} with D = 128 march_k rows
   // at pool base march_pat; march_len: planes per run (0: fill the grid)
   int march_k = 0, march_a = 0, march_pat = -1, march_len = 0;
+  // the y-march of the same pattern: K = nx / 128 slices per line, the
+  // gathered offset nx * ny (0: no y-march)
+  int ymarch_k = 0, ymarch_a = 0;
   // value-code templates (kVT): the slice table with template ids, the
   // templates (nvt x 64 words of 4-bit codes)
   const SellSlice *sl_t = nullptr;
@@ -169,6 +178,11 @@ struct CsrDev {
 // them, when the requested variant asks for them: spmv_variant keeps kVT and
 // the kernel arguments take the template slice table under exactly this
 // condition.
+// the kernel arguments walk the y-march under exactly this condition
+// (spmv_variant keeps kYM under it too)
+__host__ __device__ inline bool ym_active(const CsrDev &A) {
+  return (A.variant & kYM) && (A.variant & 2097152) && A.ymarch_k > 0 && A.march_pat >= 0;
+}
 __host__ __device__ inline bool vt_active(const CsrDev &A) {
   return (A.variant & kVT) && A.sl_t && A.vct && A.nvt > 0 && A.svc4 && A.svc && A.sl &&
          A.sell_kind && A.sell_maxw <= 8 && (A.variant & 524288) && (A.variant & 262144);

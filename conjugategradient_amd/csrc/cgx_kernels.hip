@@ -1575,13 +1575,18 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
         T g0[8], g1[8];
         const T left = wave_shr1(ccur.y, b.edge), right = wave_shl1(ccur.x, b.edge);
         constexpr int K1 = S3 ? 2 : 1;  // slot of offset -1
-        g0[0] = cprev.x;
-        g1[0] = cprev.y;
+        // z-march: slots 0 / 6 (-D, +D) from the walk, 1 / 5 (-a, +a)
+        // gathered; y-march (kYM): 1 / 5 (-nx, +nx) from the walk, 0 / 6
+        // (-nx ny, +nx ny) gathered
+        constexpr bool YM = (V & kYM) != 0;
+        constexpr int JM = YM ? 1 : 0, JG = YM ? 0 : 1;
+        g0[JM] = cprev.x;
+        g1[JM] = cprev.y;
         if constexpr (S3) {
-          g0[1] = b.gm.x;
-          g1[1] = b.gm.y;
-          g0[5] = b.gp.x;
-          g1[5] = b.gp.y;
+          g0[JG] = b.gm.x;
+          g1[JG] = b.gm.y;
+          g0[6 - JG] = b.gp.x;
+          g1[6 - JG] = b.gp.y;
         }
         g0[K1] = left;
         g1[K1] = ccur.x;
@@ -1589,8 +1594,8 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
         g1[K1 + 1] = ccur.y;
         g0[K1 + 2] = ccur.y;
         g1[K1 + 2] = right;
-        g0[W7 - 1] = cnext.x;
-        g1[W7 - 1] = cnext.y;
+        g0[W7 - 1 - JM] = cnext.x;
+        g1[W7 - 1 - JM] = cnext.y;
         epi.pre2c(r0, r0 + 1, ccur.x, ccur.y);
         T acc0 = T(0), acc1 = T(0);
 #pragma unroll
@@ -2741,6 +2746,10 @@ inline CsrArgs args(const CsrDev &A) {
             A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
             A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4,
             A.march_k, A.march_a, A.march_pat, A.march_len};
+  if (ym_active(A)) {  // the y-march walks lines of nx rows, gathers +-nx*ny
+    a.mk = A.ymarch_k;
+    a.mo = A.ymarch_a;
+  }
   if (vt_active(A)) {  // the same condition spmv_variant keeps kVT under
     a.sl = A.sl_t;
     a.vct = static_cast<const unsigned long long *>(A.vct);
@@ -3108,7 +3117,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
              (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
                    (A.sell_maxw <= 8 ? 524288 | 1048576 : 0) |
                    (A.sell_maxw <= 8 && A.march_k > 0 ? 2097152 : 0))) |
-             (vt_active(A) ? kVT : 0);
+             (vt_active(A) ? kVT : 0) | (ym_active(A) && A.sell_maxw <= 8 ? kYM : 0);
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -3200,6 +3209,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 10264578: CGX_LAUNCH_V(KERNEL, 10264578, __VA_ARGS__);\
     case 12361728: CGX_LAUNCH_V(KERNEL, 12361728, __VA_ARGS__);\
     case 12361730: CGX_LAUNCH_V(KERNEL, 12361730, __VA_ARGS__);\
+    case 20750336: CGX_LAUNCH_V(KERNEL, 20750336, __VA_ARGS__);\
+    case 20750338: CGX_LAUNCH_V(KERNEL, 20750338, __VA_ARGS__);\
+    case 29138944: CGX_LAUNCH_V(KERNEL, 29138944, __VA_ARGS__);\
+    case 29138946: CGX_LAUNCH_V(KERNEL, 29138946, __VA_ARGS__);\
     default: return hipErrorInvalidValue;                      \
   }
 
@@ -3216,7 +3229,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
   X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122) X(40978)     \
   X(106498) X(172034) X(303122) X(827410) X(9216000) X(9216002) X(10264576) X(10264578)     \
-  X(12361728) X(12361730)
+  X(12361728) X(12361730) X(20750336) X(20750338) X(29138944) X(29138946)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
 #define CGX_KP(VV) \
