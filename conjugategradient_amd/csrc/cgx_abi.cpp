@@ -2024,13 +2024,27 @@ static bool fd_auto(const cgx_cg *cg) {
 // 128^2 5.97 against 9.61 us per body in mode 4, 256^2 6.9 against 10.0,
 // 40^3 8.0 against 10.6; an irregular 100k-row matrix with longer rows
 // ties, 14.8 against 14.9 in mode 3).
+// Every workgroup of a mode-5 launch must be resident at once: one per CU at
+// most (1,024 threads hold a CU's waves; the 256-thread forms are given the
+// same bound), so the grid may not exceed the device's CUs (a partitioned
+// device mode exposes fewer than kCoopMaxG)
+static bool coop_fits(const cgx_cg *cg, int R) {
+  if (R <= 0) return false;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cg->ctx->device) !=
+      hipSuccess)
+    return false;
+  const int64_t per = (int64_t)cg->coop_nt * R;
+  return (cg->n + per - 1) / per <= cus;
+}
 static bool coop_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
   if (A->dist || cg->dtype != CGX_F64) return false;
   if (const char *e = std::getenv("CGX_AUTO_COOP")) {
     if (std::atoi(e) == 0) return false;
   }
-  return A->max_row_nnz <= kCoopK && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1;
+  return A->max_row_nnz <= kCoopK && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1 &&
+         coop_fits(cg, 1);
 }
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
@@ -2053,6 +2067,7 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) runs f64 on a single device");
     coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
+    if (coop_r > 0 && !coop_fits(cg, coop_r)) coop_r = 0;
     CGX_REQUIRE(coop_r > 0, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) takes at most %lld rows with %d threads per "
                 "workgroup (n = %lld)",
