@@ -1953,6 +1953,9 @@ template <int V> struct SpmvWaves {
   // VGPRs, a 12-byte spill) the streamed-code march gets (it took 130 and 3)
   static constexpr int w = (V & 32768) && (V & (65536 | 131072)) ? 8
                            : ((V & kVT) && (V & 2097152)) ? 4
+#ifdef CGX_VT_WAVES  // A/B: the templated consecutive walk held to more waves
+                           : ((V & kVT) && (V & 524288)) ? CGX_VT_WAVES
+#endif
                                                           : 1;
 };
 // k_spmv_fd: the same except the template march (held to 4 waves it
