@@ -2043,7 +2043,9 @@ static bool coop_auto(const cgx_cg *cg) {
   if (const char *e = std::getenv("CGX_AUTO_COOP")) {
     if (std::atoi(e) == 0) return false;
   }
-  return A->max_row_nnz <= kCoopK && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1 &&
+  // rows whose entries all sit in registers (7 in the 1,024-thread form)
+  const int kc = cg->coop_nt == 1024 ? 7 : kCoopK;
+  return A->max_row_nnz <= kc && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1 &&
          coop_fits(cg, 1);
 }
 

@@ -196,8 +196,13 @@ __device__ __forceinline__ double ld_tagged(const unsigned long long *g, int64_t
   if (trace && i >= 8 && i < 16 && t == 0)                                               \
     trace[((size_t)blockIdx.x * 8 + (i - 8)) * 8 + (ph)] = wall_clock64();
 
-// Shared prologue: this thread's rows, their first kCoopK entries, x, r, p.
+// Entries per row held in registers: kCoopK, 7 in the 1,024-thread form
+// (its 128-VGPR budget: 8 spilled 44 bytes per lane; a 7-point row fits)
+template <int NT> constexpr int coop_kc() { return NT == 1024 ? 7 : kCoopK; }
+
+// Shared prologue: this thread's rows, their first KC entries, x, r, p.
 #define CGX_COOP_PROLOGUE                                                        \
+  constexpr int KC = coop_kc<NT>();                                              \
   __shared__ double red[2][NT / 64]; /* [exchange A / B] */                      \
   __shared__ double res;                                                         \
   __shared__ int okf;                                                            \
@@ -209,15 +214,15 @@ __device__ __forceinline__ double ld_tagged(const unsigned long long *g, int64_t
   long long bodies = st->bodies;                                                 \
   int64_t row[R], rb[R];                                                         \
   int cnt[R];                                                                    \
-  int cc[R][kCoopK];                                                             \
-  double cv[R][kCoopK];                                                          \
+  int cc[R][KC];                                                             \
+  double cv[R][KC];                                                          \
   double xr[R], rv[R], pv[R];                                                    \
   _Pragma("unroll") for (int u = 0; u < R; ++u) {                                \
     row[u] = ((int64_t)blockIdx.x * R + u) * NT + t;                             \
     const bool ok = row[u] < n;                                                  \
     rb[u] = ok ? rowptr[row[u]] : 0;                                             \
     cnt[u] = ok ? rowptr[row[u] + 1] - (int)rb[u] : 0;                           \
-    _Pragma("unroll") for (int k = 0; k < kCoopK; ++k) {                         \
+    _Pragma("unroll") for (int k = 0; k < KC; ++k) {                         \
       cc[u][k] = k < cnt[u] ? col[rb[u] + k] : 0;                                \
       cv[u][k] = k < cnt[u] ? val[rb[u] + k] : 0.0;                              \
     }                                                                            \
@@ -277,9 +282,9 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
       for (int u = 0; u < R; ++u) {
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < kCoopK; ++k)
+        for (int k = 0; k < KC; ++k)
           if (k < cnt[u]) acc += cv[u][k] * ld_ag(p0 + cc[u][k]);
-        for (int k = kCoopK; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
+        for (int k = KC; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
         q[u] = acc;
       }
     } else {
@@ -292,12 +297,12 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
       for (int u = 0; u < R; ++u) {
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < kCoopK; ++k)
+        for (int k = 0; k < KC; ++k)
           if (k < cnt[u]) {
             const int j = cc[u][k];
             acc += cv[u][k] * (ld_ag(r + j) + beta * ld_ag(pprev + j));
           }
-        for (int k = kCoopK; k < cnt[u]; ++k) {
+        for (int k = KC; k < cnt[u]; ++k) {
           const int j = col[rb[u] + k];
           acc += val[rb[u] + k] * (ld_ag(r + j) + beta * ld_ag(pprev + j));
         }
@@ -367,11 +372,11 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
     unsigned long long *pg, unsigned long long *rg, CgScalars<double> *st, int slot0, int m,
     CoopWs *cw, long long ticks, unsigned long long *trace, int nap, int stall) {
   CGX_COOP_PROLOGUE
-  double gp[R][kCoopK], gr[R][kCoopK];  // this body's gathered p_{k-1}[j] (body 0: p_k) and r_k[j]
+  double gp[R][KC], gr[R][KC];  // this body's gathered p_{k-1}[j] (body 0: p_k) and r_k[j]
 #pragma unroll
   for (int u = 0; u < R; ++u)
 #pragma unroll
-    for (int k = 0; k < kCoopK; ++k) {
+    for (int k = 0; k < KC; ++k) {
       gp[u][k] = k < cnt[u] ? ld_ag(p0 + cc[u][k]) : 0.0;
       gr[u][k] = 0.0;
     }
@@ -396,14 +401,14 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
       double acc = 0.0;
       if (i == 0) {
 #pragma unroll
-        for (int k = 0; k < kCoopK; ++k)
+        for (int k = 0; k < KC; ++k)
           if (k < cnt[u]) acc += cv[u][k] * gp[u][k];
-        for (int k = kCoopK; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
+        for (int k = KC; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
       } else {
 #pragma unroll
-        for (int k = 0; k < kCoopK; ++k)
+        for (int k = 0; k < KC; ++k)
           if (k < cnt[u]) acc += cv[u][k] * (gr[u][k] + beta * gp[u][k]);
-        for (int k = kCoopK; k < cnt[u]; ++k) {
+        for (int k = KC; k < cnt[u]; ++k) {
           const int j = col[rb[u] + k];
           acc += val[rb[u] + k] * (ld_tagged(rg, j, (unsigned)i, t0, ticks, &cw->tmo) +
                                    beta * ld_tagged(pgp, j, (unsigned)i, t0, ticks, &cw->tmo));
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
 #pragma unroll
       for (int u = 0; u < R; ++u)
 #pragma unroll
-        for (int k = 0; k < kCoopK; ++k)
+        for (int k = 0; k < KC; ++k)
           if (k < cnt[u]) {
             const int j = cc[u][k];
             const unsigned long long a = ld_ag(pgc + 2 * j), b = ld_ag(pgc + 2 * j + 1);
@@ -458,7 +463,7 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
 #pragma unroll
         for (int u = 0; u < R; ++u)
 #pragma unroll
-          for (int k = 0; k < kCoopK; ++k)
+          for (int k = 0; k < KC; ++k)
             if (k < cnt[u]) {
               gp[u][k] = ld_tagged(pgc, cc[u][k], tag, t1, ticks, &cw->tmo);
               gr[u][k] = ld_tagged(rg, cc[u][k], tag, t1, ticks, &cw->tmo);
