@@ -369,6 +369,11 @@ constexpr bool kStreamNt = true;
 #ifndef CGX_NT_VEC_BYTES
 #define CGX_NT_VEC_BYTES (int64_t(32) << 20)
 #endif
+// loads in flight per thread and trip in k_update_r (A/B: -DCGX_UPDATE_R_UNROLL=8)
+#ifndef CGX_UPDATE_R_UNROLL
+#define CGX_UPDATE_R_UNROLL 4
+#endif
+constexpr int kUR = CGX_UPDATE_R_UNROLL;
 template <typename T> __device__ __forceinline__ bool stream_nt(int64_t n) {
   return kStreamNt && n * (int64_t)sizeof(T) > CGX_NT_VEC_BYTES;
 }
@@ -2236,9 +2241,9 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   T pl[kPartsPerThread];
   const bool from_parts = !FUSED && np_pap > 0;
   if (from_parts) parts_load(ws->pap_part, np_pap, pl);
-  V rv[4], av[4];
+  V rv[kUR], av[kUR];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {  // clamped (r and Ap have a slack element): no branch
+  for (int u = 0; u < kUR; ++u) {  // clamped (r and Ap have a slack element): no branch
     const int64_t j = E(min(i + u * stride, n2 > 0 ? n2 - 1 : 0));
     rv[u] = ri2[j];
     av[u] = ldv<SNT, T>(a2 + j);  // Ap is dead after this kernel
@@ -2285,16 +2290,16 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     }
   }
   T acc = T(0);
-  for (bool first = true; i + 3 * stride < n2; i += 4 * stride, first = false) {
+  for (bool first = true; i + (kUR - 1) * stride < n2; i += kUR * stride, first = false) {
     if (!first) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kUR; ++u) {
         rv[u] = ri2[E(i + u * stride)];
         av[u] = ldv<SNT, T>(a2 + E(i + u * stride));
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kUR; ++u) {
       rv[u].x = rv[u].x - alpha * av[u].x;
       rv[u].y = rv[u].y - alpha * av[u].y;
       r2[E(i + u * stride)] = rv[u];
