@@ -395,7 +395,8 @@ int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
   const CsrDev &A = cg->A->dev;
   const int m = (int)std::min<int64_t>(bodies, 1 << 30);
   return timed(cg, 1, cg->ctx->stream, [&] {
-    return cg_coop(cg->n, cg->coop_r, cg->coop_nt, cg->coop_tagr, A.rowptr, A.col, (const double *)A.val,
+    return cg_coop(cg->n, cg->coop_r, cg->coop_stream ? 1024 : cg->coop_nt,
+                   cg->coop_stream ? 2 : cg->coop_tagr ? 1 : 0, A.rowptr, A.col, (const double *)A.val,
                    (double *)cg->x, (double *)cg->r, (double *)cg->p, (double *)cg->p2,
                    (unsigned long long *)cg->coop_rg, (CgScalars<double> *)cg->st, slot, m,
                    (CoopWs *)cg->coop_ws, cg->coop_ticks,
@@ -2028,14 +2029,42 @@ static bool fd_auto(const cgx_cg *cg) {
 // most (1,024 threads hold a CU's waves; the 256-thread forms are given the
 // same bound), so the grid may not exceed the device's CUs (a partitioned
 // device mode exposes fewer than kCoopMaxG)
-static bool coop_fits(const cgx_cg *cg, int R) {
-  if (R <= 0) return false;
+static int device_cus(const cgx_cg *cg) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cg->ctx->device) !=
       hipSuccess)
-    return false;
+    return 0;
+  return cus;
+}
+static bool coop_fits(const cgx_cg *cg, int R) {
+  if (R <= 0) return false;
   const int64_t per = (int64_t)cg->coop_nt * R;
-  return (cg->n + per - 1) / per <= cus;
+  return (cg->n + per - 1) / per <= device_cus(cg);
+}
+// The streamed form (2): rows of any length, R <= 8 rows per thread of
+// 1,024-thread workgroups, one per CU at most
+static int coop_stream_r(const cgx_cg *cg) {
+  return coop_stream_rows(cg->n, coop_want_r(), device_cus(cg));
+}
+// auto: where neither register form applies (rows past 7 entries, or past
+// kCoopMaxGReg workgroups), the matrix is on the CSR-stream path (it has no
+// SELL copy: the stencils' SELL-P / value-code bodies win there) and the
+// streamed form fits with at most kCoopStreamAutoR rows per thread — where
+// it was measured to win (profiles/r03_coop_stream.log: irregular 100k /
+// 200k / 400k rows 11.2 / 12.5 / 18.9 us per body against 14.3 / 16.6 /
+// 19.6 in mode 3; at 4 and more rows per thread, and on the stencils, the
+// three-kernel bodies are faster). $CGX_COOP_STREAM=0: never; 1: whenever
+// it fits.
+constexpr int kCoopStreamAutoR = 2;
+static bool coop_stream_auto(const cgx_cg *cg) {
+  const cgx_csr *A = cg->A;
+  if (A->dist || cg->dtype != CGX_F64 || cg->coop_stream_want == 0) return false;
+  if (const char *e = std::getenv("CGX_AUTO_COOP"); e && std::atoi(e) == 0) return false;
+  const int R = coop_stream_r(cg);
+  if (R <= 0) return false;
+  if (cg->coop_stream_want == 1) return true;
+  const bool csr_path = !A->dev.sl;  // no SELL copy: the SpMV is CSR-stream
+  return csr_path && R <= kCoopStreamAutoR;
 }
 static bool coop_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
@@ -2064,17 +2093,26 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
     cg->coop_stall = -1;
     if (const char *e = std::getenv("CGX_COOP_INJECT_STALL")) cg->coop_stall = std::atoi(e);
+    cg->coop_stream_want = -1;
+    if (const char *e = std::getenv("CGX_COOP_STREAM")) cg->coop_stream_want = std::atoi(e);
   }
+  bool stream = false;
   if (mode == 5) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) runs f64 on a single device");
-    coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
-    if (coop_r > 0 && !coop_fits(cg, coop_r)) coop_r = 0;
+    if (cg->coop_stream_want != 1) {
+      coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
+      if (coop_r > 0 && !coop_fits(cg, coop_r)) coop_r = 0;
+    }
+    if (coop_r == 0 && cg->coop_stream_want != 0) {
+      coop_r = coop_stream_r(cg);
+      stream = coop_r > 0;
+    }
     CGX_REQUIRE(coop_r > 0, CGX_EUNSUPPORTED,
-                "mode 5 (persistent body) takes at most %lld rows with %d threads per "
-                "workgroup (n = %lld)",
-                (long long)kCoopMaxG * cg->coop_nt * (cg->coop_nt == 256 ? 4 : 1),
-                cg->coop_nt, (long long)cg->n);
+                "mode 5 (persistent body) takes at most %lld rows (%d workgroups of 1024 "
+                "threads, %d rows per thread; n = %lld)",
+                (long long)std::min(device_cus(cg), kCoopMaxG) * 1024 * kCoopStreamMaxR,
+                std::min(device_cus(cg), kCoopMaxG), kCoopStreamMaxR, (long long)cg->n);
   }
   CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
               "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
@@ -2088,7 +2126,13 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   if (mode == 0) {
     mode = coop_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
     if (mode == 5) coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
-    if (mode == 5 && coop_r == 0) mode = fd_auto(cg) ? 4 : 3;
+    if (mode != 5 || coop_r == 0) {
+      mode = coop_stream_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
+      if (mode == 5) {
+        coop_r = coop_stream_r(cg);
+        stream = true;
+      }
+    }
   }
   const bool f = mode == 2, d = mode == 3, fd = mode == 4, c = mode == 5;
   if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop) {
@@ -2113,7 +2157,10 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
       cg->coop_ticks = (long long)clk_khz * std::max(1, std::atoi(e));
   }
   cg->coop = c;
-  if (c) cg->coop_r = coop_r;
+  if (c) {
+    cg->coop_r = coop_r;
+    cg->coop_stream = stream;
+  }
   if ((d || fd) && !cg->pk[0]) {  // three more p buffers (with the ghost tail when partitioned)
     DeviceGuard g(cg->ctx->device);
     const size_t bytes = (size_t)(cg->n + cg->A->halo.n_ghost) * dtype_size(cg->dtype);
@@ -2378,10 +2425,10 @@ extern "C" int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads,
               "NULL argument");
   CGX_REQUIRE(cg->coop, CGX_ESTATE, "the solver is not in mode 5");
   *rows_per_thread = cg->coop_r;
-  *threads = cg->coop_nt;
-  const int64_t per = (int64_t)cg->coop_nt * cg->coop_r;
+  *threads = cg->coop_stream ? 1024 : cg->coop_nt;
+  const int64_t per = (int64_t)*threads * cg->coop_r;
   *workgroups = (int)((cg->n + per - 1) / per);
-  *tagged = cg->coop_tagr ? 1 : 0;
+  *tagged = cg->coop_stream ? 2 : cg->coop_tagr ? 1 : 0;
   return CGX_OK;
 }
 

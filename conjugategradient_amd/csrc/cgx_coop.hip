@@ -43,6 +43,8 @@
 // (CgScalars::stopped = 4).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "cgx_internal.h"
 
 namespace cgx {
@@ -106,32 +108,29 @@ __device__ __forceinline__ void publish(unsigned long long *gran, double part, u
 }
 
 // Every workgroup: wave 0 sweeps all G partials until every tag is `tag`,
-// sums them in workgroup order (lane l: partials l, l + 64; then the wave's
-// shuffle tree), broadcasts through LDS. false: a spin gave up.
+// sums them in workgroup order (lane l: partials l, l + 64, l + 128, l + 192;
+// then the wave's shuffle tree), broadcasts through LDS. false: a spin gave up.
 __device__ __forceinline__ bool collect(const unsigned long long *gran, unsigned tag,
                                         long long ticks, unsigned *tmo, double *res_lds,
                                         int *ok_lds, int nap) {
   const int G = gridDim.x;
-  static_assert(kCoopMaxG <= 128, "collect reads two partials per lane");
+  static_assert(kCoopMaxG <= 256, "collect reads four partials per lane");
   if (threadIdx.x < 64) {
     const int l = threadIdx.x;
     double v = 0.0;
     bool ok = true;
     const long long t0 = wall_clock64();
-    // kCoopMaxG <= 128: lane l holds partials l and l + 64, read in one pass
-    const bool m0 = l < G, m1 = l + 64 < G;
-    unsigned long long a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+    // lane l holds partials l + 64 q (q < 4), read in one pass
+    unsigned long long a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     for (;;) {
       bool got = true;
-      if (m0) {
-        a0 = ld_ag(gran + 2 * l);
-        b0 = ld_ag(gran + 2 * l + 1);
-        got = (unsigned)(a0 >> 32) == tag && (unsigned)(b0 >> 32) == tag;
-      }
-      if (m1) {
-        a1 = ld_ag(gran + 2 * (l + 64));
-        b1 = ld_ag(gran + 2 * (l + 64) + 1);
-        got = got && (unsigned)(a1 >> 32) == tag && (unsigned)(b1 >> 32) == tag;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (l + 64 * q < G) {
+          a[q] = ld_ag(gran + 2 * (l + 64 * q));
+          b[q] = ld_ag(gran + 2 * (l + 64 * q) + 1);
+          got = got && (unsigned)(a[q] >> 32) == tag && (unsigned)(b[q] >> 32) == tag;
+        }
       }
       if (__all(got)) break;
       const bool late = wall_clock64() - t0 > ticks ||
@@ -143,8 +142,11 @@ __device__ __forceinline__ bool collect(const unsigned long long *gran, unsigned
       for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(1);
     }
     if (ok) {
-      if (m0) v = __longlong_as_double((long long)((a0 & 0xffffffffull) | ((b0 & 0xffffffffull) << 32)));
-      if (m1) v += __longlong_as_double((long long)((a1 & 0xffffffffull) | ((b1 & 0xffffffffull) << 32)));
+      if (l < G) v = __longlong_as_double((long long)((a[0] & 0xffffffffull) | ((b[0] & 0xffffffffull) << 32)));
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (l + 64 * q < G)
+          v += __longlong_as_double((long long)((a[q] & 0xffffffffull) | ((b[q] & 0xffffffffull) << 32)));
     }
     v = wave_sum(v);
     if (l == 0) {
@@ -493,6 +495,201 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
   coop_gave_up(st);
 }
 
+// Form 2 (streamed, problems past the register forms: more rows than
+// kCoopMaxGReg x 1,024, or rows longer than 7 entries): 1,024 threads, R rows
+// per thread, r of the rows in registers, x and p in LDS (the 128-VGPR
+// budget of 16 waves per CU), the matrix read every body. Chunk u of
+// workgroup g is rows [(g R + u) 1024, + 1024), whose entries are
+// contiguous: the workgroup's threads load them coalesced (entry e by thread
+// e mod 1024, four per pass in flight), form each product
+// val[e] * p_k[col[e]] (p_k[j] = r_k[j] + beta p_{k-1}[j], as form 0) and
+// stage it in LDS; thread t then sums its row's products in ascending entry
+// order from 0 — the reference's row loop, bit for bit. A chunk of more than
+// coop_stage<R>() entries (long rows) is summed by its row threads from the
+// CSR arrays instead. Exchanges, updates and the record as form 0.
+constexpr int kCoopStP = 5;  // streamed form: entries per thread of a one-pass chunk
+template <int R> constexpr int coop_stage() { return (160 * 1024 - R * 1024 * 16 - 1024) / 8; }
+template <int R>
+__global__ __launch_bounds__(1024, 1) void k_cg_coop_st(
+    int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const double *__restrict__ val, double *__restrict__ x, double *r, double *p0, double *p1,
+    CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks,
+    unsigned long long *trace, int nap, int stall) {
+  constexpr int NT = 1024, C = coop_stage<R>();
+  __shared__ double stage[C];
+  __shared__ double xs[R][NT];  // this workgroup's x
+  __shared__ double ps[R][NT];  // and p (p_k of its rows)
+  __shared__ double red[2][NT / 64];
+  __shared__ double res;
+  __shared__ int okf;
+  if (!st->active[slot0]) return;
+  const int t = threadIdx.x;
+  double rxr = st->rxr[slot0];
+  const double tol = st->tol;
+  const long long cap = st->cap;
+  long long bodies = st->bodies;
+  // row u of this thread: (g R + u) 1024 + tq; tq is re-made opaque every
+  // body so the compiler re-forms the row addresses instead of holding R of
+  // them (64-bit) across the body loop
+  int tq = t, gq = blockIdx.x;
+  auto rowid = [&](int u) { return ((int64_t)gq * R + u) * NT + tq; };
+  // per row: its first entry's offset in its chunk << 16 | its entry count
+  // (chunks of at most C entries; others take the CSR path)
+  unsigned oc[R];
+  double rv[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int64_t f = ((int64_t)blockIdx.x * R + u) * NT, w = rowid(u);
+    const bool ok = w < n;
+    const int b0 = f < n ? rowptr[f] : 0;
+    const int rb = ok ? rowptr[w] : 0;
+    oc[u] = ok ? ((unsigned)(rb - b0) << 16) | (unsigned)(rowptr[w + 1] - rb) : 0u;
+    xs[u][t] = ok ? x[w] : 0.0;
+    rv[u] = ok ? r[w] : 0.0;
+    ps[u][t] = ok ? p0[w] : 0.0;
+  }
+  double beta = 0.0;
+  for (int i = 0; i < m; ++i) {
+    const int s = (slot0 + i) & 3;
+    const unsigned tag = (unsigned)i + 1u;
+    asm volatile("" : "+v"(tq), "+s"(gq));
+    CGX_COOP_TR(0)
+    double *pcur = (i & 1) ? p1 : p0;
+    const double *pprev = (i & 1) ? p0 : p1;
+    if (i > 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const double pu = rv[u] + beta * ps[u][t];  // p = r + beta p (CG.hpp:418), own rows
+        ps[u][t] = pu;
+        if (rowid(u) < n) st_ag(pcur + rowid(u), pu);
+      }
+    }
+    // p_k[j] as every reader forms it, r_k[j] + beta p_{k-1}[j]; the launch's
+    // first body reads p_k itself (p_k[j] + 0 p_k[j]: the same value for
+    // finite p) — no branch between the gathers of a pass
+    const double *ga = i == 0 ? p0 : r, *gb = i == 0 ? p0 : pprev;
+    const double bk = i == 0 ? 0.0 : beta;
+    auto pk = [&](int j) { return ld_ag(ga + j) + bk * ld_ag(gb + j); };
+    double q[R];
+    // chunk u's entries [base, base + E)
+    auto span = [&](int u, int &base, int &E) {
+      const int64_t f = ((int64_t)gq * R + u) * NT;
+      base = f < n ? rowptr[f] : 0;
+      E = f < n ? rowptr[f + NT < n ? f + NT : n] - base : 0;
+    };
+    // a chunk of at most PW entries is one pass of P per thread, its col/val
+    // loaded while the previous chunk's gathers are in flight
+    constexpr int P = kCoopStP, PW = P * NT < C ? P * NT : C;
+    int jj[P];
+    double vv[P];
+    auto load = [&](int base, int E) {
+#pragma unroll
+      for (int z = 0; z < P; ++z) {  // clamped: no branch before the loads
+        const int e = min(z * NT + t, E - 1);
+        jj[z] = col[base + e];
+        vv[z] = val[base + e];
+      }
+    };
+    int bn, en;
+    span(0, bn, en);
+    if (en > 0 && en <= PW) load(bn, en);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int base = bn, E = en;
+      double acc = 0.0;
+      double pr[P];
+      if (E <= PW) {
+#pragma unroll
+        for (int z = 0; z < P; ++z) pr[z] = vv[z] * pk(jj[z]);
+      }
+      if (u + 1 < R) {
+        span(u + 1, bn, en);
+        if (en > 0 && en <= PW) load(bn, en);
+      }
+      if (E <= C) {
+        if (E <= PW) {
+#pragma unroll
+          for (int z = 0; z < P; ++z)
+            if (z * NT + t < E) stage[z * NT + t] = pr[z];
+        } else {
+#pragma unroll 1
+          for (int s0 = 0; s0 < E; s0 += 4 * NT) {
+            int j4[4];
+            double v4[4], p4[4];
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+              const int e = min(s0 + z * NT + t, E - 1);
+              j4[z] = col[base + e];
+              v4[z] = val[base + e];
+            }
+#pragma unroll
+            for (int z = 0; z < 4; ++z) p4[z] = v4[z] * pk(j4[z]);
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+              const int e = s0 + z * NT + t;
+              if (e < E) stage[e] = p4[z];
+            }
+          }
+        }
+        __syncthreads();
+        const int o = (int)(oc[u] >> 16), c = (int)(oc[u] & 0xffffu);
+        for (int k = 0; k < c; ++k) acc += stage[o + k];
+        __syncthreads();  // the next chunk overwrites the stage
+      } else if (rowid(u) < n) {  // long rows in the chunk: every row from the CSR arrays
+        const int rb = rowptr[rowid(u)], re = rowptr[rowid(u) + 1];
+#pragma unroll 1
+        for (int k = rb; k < re; ++k) acc += val[k] * pk(col[k]);
+      }
+      q[u] = acc;
+    }
+    CGX_COOP_TR(1)
+    // p.Ap (CG.hpp:374-379)
+    double part = 0.0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) part += ps[u][t] * q[u];
+    drain();  // this wave's p stores are out before the workgroup publishes
+    part = block_sum<NT>(part, red[0]);
+    CGX_COOP_TR(2)
+    if (!(i == stall && blockIdx.x == 0)) publish(cw->ga, part, tag);
+    if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(3)
+    const double pAp = res;
+    const double alpha = rxr / pAp;
+    // x += alpha p; r -= alpha Ap; r.r   (CG.hpp:381-393, 406-407)
+    part = 0.0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      xs[u][t] = xs[u][t] + alpha * ps[u][t];
+      rv[u] = rv[u] - alpha * q[u];
+      if (rowid(u) < n) st_ag(r + rowid(u), rv[u]);
+      part += rv[u] * rv[u];
+    }
+    drain();
+    part = block_sum<NT>(part, red[1]);
+    CGX_COOP_TR(4)
+    publish(cw->gb, part, tag);
+    CGX_COOP_TR(5)
+    if (!collect(cw->gb, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
+    CGX_COOP_TR(6)
+    const double rr = res;
+    ++bodies;
+    const bool cont = coop_record(st, s, pAp, rr, alpha, rxr, tol, bodies, cap);
+    beta = rr / rxr;
+    rxr = rr;
+    if (!cont || i == m - 1) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (rowid(u) < n) {
+          p0[rowid(u)] = rv[u] + beta * ps[u][t];  // p_{k+1}, and x, in the standard buffers
+          x[rowid(u)] = xs[u][t];
+        }
+      }
+      return;
+    }
+  }
+  coop_gave_up(st);
+}
+
 }  // namespace
 
 int coop_rows_per_thread(int64_t n, int want, int nt) {
@@ -502,18 +699,29 @@ int coop_rows_per_thread(int64_t n, int want, int nt) {
     if (want > 0 && R != want) continue;
     if (nt == 1024 && R != 1) continue;  // 128 VGPRs at 16 waves per CU
     if (nt == 512 && R > 2) continue;    // <4, 512> spills
-    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= kCoopMaxG) return R;
+    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= kCoopMaxGReg) return R;
   }
   return 0;
 }
 
-hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
+int coop_stream_rows(int64_t n, int want, int max_g) {
+  for (int R = 1; R <= kCoopStreamMaxR; ++R) {
+    if (want > 0 && R != want) continue;
+    if ((n + 1024LL * R - 1) / (1024LL * R) <= std::min(max_g, kCoopMaxG)) return R;
+  }
+  return 0;
+}
+
+hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
                    unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
                    long long ticks, unsigned long long *trace, int nap, int stall,
                    hipStream_t s) {
   const int G = (int)((n + (int64_t)NT * R - 1) / ((int64_t)NT * R));
+  const bool tagged = form == 1;
   if (G < 1 || G > kCoopMaxG || m < 1 || (tagged && !g)) return hipErrorInvalidValue;
+  if (form == 2 && (NT != 1024 || R < 1 || R > kCoopStreamMaxR)) return hipErrorInvalidValue;
+  if (form != 2 && G > kCoopMaxGReg) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
   if (e == hipSuccess && tagged) e = hipMemsetAsync(g, 0, (size_t)n * 48, s);
   if (e != hipSuccess) return e;
@@ -524,6 +732,20 @@ hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, con
 #define CGX_COOP_TG(RR, TT)                                                                 \
   k_cg_coop_tg<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, pg, rg, st, slot0, m, \
                                         cw, ticks, trace, nap, stall)
+#define CGX_COOP_ST(RR)                                                                     \
+  case RR:                                                                                  \
+    k_cg_coop_st<RR><<<G, 1024, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
+                                        ticks, trace, nap, stall);                          \
+    break;
+  if (form == 2) {
+    switch (R) {
+      CGX_COOP_ST(1) CGX_COOP_ST(2) CGX_COOP_ST(3) CGX_COOP_ST(4)
+      CGX_COOP_ST(5) CGX_COOP_ST(6) CGX_COOP_ST(7) CGX_COOP_ST(8)
+      default: return hipErrorInvalidValue;
+    }
+#undef CGX_COOP_ST
+    return hipGetLastError();
+  }
   const int key = (NT == 1024 ? 100 : NT == 512 ? 50 : 0) + R * 2 + (tagged ? 1 : 0);
   switch (key) {
     case 2: CGX_COOP_WT(1, 256); break;

@@ -293,7 +293,8 @@ enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 
 // ---- persistent CG body (mode 5, cgx_coop.hip) -------------------------------
 constexpr int kCoopK = 8;       // entries per row held in registers
-constexpr int kCoopMaxG = 128;  // workgroups: at most one per CU on half the chip
+constexpr int kCoopMaxG = 256;     // workgroups: at most one per CU (exchange granules)
+constexpr int kCoopMaxGReg = 128;  // the register forms: at most one per CU on half the chip
 // exchange granules ({tag, half of a double}: two per workgroup and exchange),
 // zeroed before every launch
 struct CoopWs {
@@ -303,16 +304,20 @@ struct CoopWs {
   unsigned int pad[3];
 };
 // rows per thread (1, 2 or 4; `want` > 0 asks for one) for which n rows fit
-// kCoopMaxG workgroups of nt threads (256, or 1024 with one row per
+// kCoopMaxGReg workgroups of nt threads (256, or 1024 with one row per
 // thread); 0: none
 int coop_rows_per_thread(int64_t n, int want, int nt);
+// the streamed form (2): the least R <= kCoopStreamMaxR for which n rows fit
+// min(max_g, kCoopMaxG) workgroups of 1,024 threads; 0: none
+constexpr int kCoopStreamMaxR = 8;
+int coop_stream_rows(int64_t n, int want, int max_g);
 // up to m bodies from slot0 in one launch (f64, single device): x, r, p0 in
 // and out in the standard layout, p1 scratch (n entries); stops as the
 // three-kernel body does, or sets st->stopped = 4 when a spin gave up
-// tagged (form 1): p and r handed over as tagged granules in g (6 n words:
-// two p copies, then r), else (form 0) drained write-through stores into r,
-// p0 and p1
-hipError_t cg_coop(int64_t n, int R, int NT, bool tagged, const int *rowptr, const int *col,
+// form 1 (tagged): p and r handed over as tagged granules in g (6 n words:
+// two p copies, then r); forms 0 and 2: drained write-through stores into r,
+// p0 and p1; form 2 (streamed, NT = 1024) reads the matrix every body
+hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
                    unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
                    long long ticks, unsigned long long *trace, int nap, int stall,

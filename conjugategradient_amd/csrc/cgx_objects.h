@@ -191,6 +191,8 @@ struct cgx_cg {
   void *coop_ws = nullptr;  // cgx::CoopWs
   void *coop_rg = nullptr;  // tagged p and r granules (6 n words; $CGX_COOP_TAGR=1)
   bool coop_tagr = false;
+  bool coop_stream = false;  // form 2: the matrix read every body (k_cg_coop_st)
+  int coop_stream_want = -1; // $CGX_COOP_STREAM: -1 auto, 0 never, 1 always
   void *coop_trace = nullptr;  // $CGX_COOP_TRACE: phase stamps (cgx_cg_coop_trace)
   long long coop_ticks = 0; // wall-clock ticks before an exchange spin gives up
   bool altdir = false;  // alternate the kernels' sweep directions (Infinity-Cache reuse)

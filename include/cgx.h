@@ -187,16 +187,20 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * beta p_{k-1} computed where the SpMV reads it and stored once into the
  * p ring, update_r with the stop rule, x from the four p buffers in slot 3
  * (72 N + matrix bytes per body against 78 N in mode 3); 5 persistent body
- * (single device, f64, n <= 131072 rows): one launch runs a whole chunk of
+ * (single device, f64; register forms up to 131072 rows, the streamed form
+ * up to 8 x 1024 x min(256, CUs) rows): one launch runs a whole chunk of
  * bodies, each with two grid-wide exchanges of the dot partials instead of
  * three kernel boundaries; Ap bit-identical, the dots summed in another
- * order (x equal to rounding). $CGX_COOP_R picks its rows per thread.
+ * order (x equal to rounding). $CGX_COOP_R picks its rows per thread,
+ * $CGX_COOP_STREAM=1 / 0 always / never the streamed form.
  * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
  * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
 /* mode 5's launch shape: rows per thread, threads per workgroup ($CGX_COOP_NT,
- * default 1024), workgroups, 1 when p and r are handed over as tagged
- * granules ($CGX_COOP_TAGR=1; default 0: drained write-through stores) */
+ * default 1024), workgroups, and the form: 0 register form with drained
+ * write-through stores (default), 1 register form with p and r handed over
+ * as tagged granules ($CGX_COOP_TAGR=1), 2 the streamed form (the matrix
+ * read every body, entries staged through LDS) */
 int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads, int *workgroups,
                       int *tagged);
 /* diagnostics: with $CGX_COOP_TRACE=1 set before mode 5 is chosen, the

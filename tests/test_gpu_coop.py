@@ -17,7 +17,14 @@ from tests.util import irregular_spd, rel
 pytestmark = pytest.mark.gpu
 
 
-def _solve(queue, m, b, mode, tol, max_iter=-1, x0=None, poll=32):
+def _shape(h):
+    """(rows per thread, threads, workgroups, form) of a mode-5 solver"""
+    v = [C.c_int() for _ in range(4)]
+    check(lib().cgx_cg_coop_shape(h, *[C.byref(a) for a in v]))
+    return tuple(a.value for a in v)
+
+
+def _solve(queue, m, b, mode, tol, max_iter=-1, x0=None, poll=32, shape=None):
     cg = cga.CG(queue)
     cg.mode = mode
     cg.poll_every = poll
@@ -26,6 +33,8 @@ def _solve(queue, m, b, mode, tol, max_iter=-1, x0=None, poll=32):
     if x0 is not None:
         cg.setInital(x0)
     cg.solve(tol, max_iter=max_iter)
+    if shape is not None:
+        shape.append(_shape(cg._cg))
     return cg.extract(), cg.iterations, cg.final_rxr
 
 
@@ -51,6 +60,72 @@ def test_mode5_fixed_bodies_match_oracle(queue, oracle, monkeypatch, dims, R, NT
     assert rel(x5, x1) <= 1e-11 and r5 == pytest.approx(r1, rel=1e-9)
     _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 45, 8)
     assert rel(x5, xr) <= 1e-10
+
+
+@pytest.mark.parametrize("R", ["1", "2", "3"])
+@pytest.mark.parametrize("dims", [(2, 128, 128, 1), (3, 20, 18, 17), (2, 70, 66, 1)],
+                         ids=["p2d_128", "p3d_20x18x17", "p2d_70x66"])
+def test_mode5_streamed_fixed_bodies_match_oracle(queue, oracle, monkeypatch, dims, R):
+    """The streamed form ($CGX_COOP_STREAM=1): R rows per thread of 1,024,
+    the matrix's entries staged through LDS chunk by chunk."""
+    monkeypatch.setenv("CGX_COOP_STREAM", "1")
+    monkeypatch.setenv("CGX_COOP_R", R)
+    rp, cl, vl = oracle.poisson(*dims)
+    n = len(rp) - 1
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    shape = []
+    x5, it5, r5 = _solve(queue, m, b, 5, 0.0, max_iter=45, shape=shape)
+    assert shape[0][0] == int(R) and shape[0][1] == 1024 and shape[0][3] == 2
+    assert shape[0][2] == -(-n // (1024 * int(R)))
+    x1, it1, r1 = _solve(queue, m, b, 1, 0.0, max_iter=45)
+    assert it5 == it1 == 45
+    assert rel(x5, x1) <= 1e-11 and r5 == pytest.approx(r1, rel=1e-9)
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 45, 8)
+    assert rel(x5, xr) <= 1e-10
+
+
+def test_mode5_streamed_long_rows_and_tolerance(queue, oracle, monkeypatch):
+    """A chunk with more entries than the LDS stage (a hub row of 30,000
+    entries) is summed from the CSR arrays; to tolerance and warm, with the
+    stop inside and at the end of launches."""
+    monkeypatch.setenv("CGX_COOP_STREAM", "1")
+    rp, cl, vl = irregular_spd(40000, seed=4, hub=30000, shift=10.0)
+    assert np.diff(rp).max() > 20000
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    x5, it5, _ = _solve(queue, m, b, 5, 0.0, max_iter=30)
+    assert it5 == 30
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 30, 8)
+    assert rel(x5, xr) <= 1e-10
+    rp, cl, vl = oracle.poisson(3, 16, 15, 14)
+    n = len(rp) - 1
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    x0 = np.random.default_rng(2).standard_normal(n)
+    for start in (None, x0):
+        for poll in (1, 32):
+            t = 1e-8 * np.linalg.norm(b)
+            x5, it5, _ = _solve(queue, m, b, 5, t, x0=start, poll=poll)
+            x1, it1, _ = _solve(queue, m, b, 1, t, x0=start)
+            assert abs(it5 - it1) <= 2 and rel(x5, x1) <= 1e-9
+
+
+def test_mode5_streamed_g3_standin(queue, oracle, monkeypatch):
+    """The G3_circuit stand-in (1,585,478 rows) in the streamed
+    form: 7 rows per thread, 222 workgroups; 20 bodies against mode 3."""
+    from conjugategradient_amd import workloads
+    monkeypatch.setenv("CGX_COOP_STREAM", "1")
+    rp, cl, vl = workloads.host_csr("g3_standin")
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    shape = []
+    x5, it5, r5 = _solve(queue, m, b, 5, 0.0, max_iter=20, shape=shape)
+    assert shape[0][3] == 2
+    x3, it3, r3 = _solve(queue, m, b, 3, 0.0, max_iter=20)
+    assert it5 == it3 == 20
+    print("g3 streamed vs mode 3: rel", rel(x5, x3), "shape", shape[0])
+    assert rel(x5, x3) <= 1e-8
 
 
 def test_mode5_solves_to_tolerance_and_warm_start(queue, oracle):
@@ -116,12 +191,34 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
         assert b"mode 5" in L.cgx_last_error()
     finally:
         L.cgx_cg_destroy(h)
-    big = cga.Matrix.poisson(queue, 3, 64, 64, 40)  # 163,840 rows
+    # past the streamed form: 8 rows x 1,024 threads x 256 workgroups
+    big = cga.Matrix.poisson(queue, 3, 130, 130, 130)  # 2,197,000 rows
     check(L.cgx_cg_create(queue.handle, big.schedule(), C.byref(h)))
     try:
         assert L.cgx_cg_set_mode(h, 5) != 0
+        assert b"at most" in L.cgx_last_error()
     finally:
         L.cgx_cg_destroy(h)
+    del big
+    # past the register forms: the streamed form; in auto only on the
+    # CSR-stream path at <= 2 rows per thread (an irregular 200k-row matrix,
+    # not a 3-D stencil of 163,840 rows, not 1,000,000 rows)
+    rp, cl, vl = irregular_spd(200000, seed=5)
+    cases = ((lambda: cga.Matrix(queue, vl, cl, rp), True),
+             (lambda: cga.Matrix.poisson(queue, 3, 64, 64, 40), False),
+             (lambda: cga.Matrix.poisson(queue, 3, 100, 100, 100), False))
+    for make, auto5 in cases:
+        mid = make()
+        check(L.cgx_cg_create(queue.handle, mid.schedule(), C.byref(h)))
+        try:
+            check(L.cgx_cg_set_mode(h, 0))
+            mode = C.c_int()
+            check(L.cgx_cg_get_mode(h, C.byref(mode)))
+            assert (mode.value == 5) == auto5
+            check(L.cgx_cg_set_mode(h, 5))
+            assert _shape(h)[3] == 2
+        finally:
+            L.cgx_cg_destroy(h)
 
 
 @pytest.mark.parametrize("tagr", ["0", "1"])
@@ -145,7 +242,8 @@ def test_mode5_r_handoff_forms(queue, oracle, monkeypatch, tagr):
     assert rel(x5, xr) <= 1e-10
 
 
-def test_mode5_stalled_exchange_times_out_and_recovers(queue, oracle, monkeypatch):
+@pytest.mark.parametrize("stream", ["0", "1"])
+def test_mode5_stalled_exchange_times_out_and_recovers(queue, oracle, monkeypatch, stream):
     """Every spin of the persistent body is bounded: with workgroup 0
     withholding one body's p.Ap partial (fault injection), the others give
     up after $CGX_COOP_TIMEOUT_MS and raise the shared flag, the launch ends,
@@ -155,6 +253,7 @@ def test_mode5_stalled_exchange_times_out_and_recovers(queue, oracle, monkeypatc
     n = len(rp) - 1
     m = cga.Matrix(queue, vl, cl, rp)
     b = np.arange(1, n + 1, dtype=np.float64)
+    monkeypatch.setenv("CGX_COOP_STREAM", stream)
     monkeypatch.setenv("CGX_COOP_INJECT_STALL", "3")
     monkeypatch.setenv("CGX_COOP_TIMEOUT_MS", "50")
     with pytest.raises(Exception, match="mode 5"):

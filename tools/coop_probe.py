@@ -23,6 +23,15 @@ CONFIGS = {
     "p3d_32": lambda: ("poisson", (3, 32, 32, 32)),
     "p3d_40": lambda: ("poisson", (3, 40, 40, 40)),
     "irr_100k": lambda: ("irr", 100000),
+    "irr_400k": lambda: ("irr", 400000),
+    "p2d_512": lambda: ("poisson", (2, 512, 512, 1)),
+    "p2d_1024": lambda: ("poisson", (2, 1024, 1024, 1)),
+    "p3d_100": lambda: ("poisson", (3, 100, 100, 100)),
+    "p3d_164k": lambda: ("poisson", (3, 64, 64, 40)),
+    "p3d_80": lambda: ("poisson", (3, 80, 80, 80)),
+    "p2d_700": lambda: ("poisson", (2, 700, 700, 1)),
+    "irr_200k": lambda: ("irr", 200000),
+    "g3": lambda: ("g3", None),
 }
 
 
@@ -35,8 +44,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--shapes", default="", help="R:tagged:threads,... (mode 5 shapes to time)")
+    ap.add_argument("--shapes", default="", help="R:form:threads,... (mode 5 shapes to time; "
+                    "form 0 write-through, 1 tagged, 2 streamed; R 0: the fewest that fit)")
+    ap.add_argument("--base-env", default="", help="K=V,... for the mode-0 runs (e.g. "
+                    "CGX_COOP_STREAM=0: the auto mode without the streamed form)")
     a = ap.parse_args()
+    base_env = dict(kv.split("=", 1) for kv in a.base_env.split(",") if kv)
     global VARIANTS
     if a.shapes:
         VARIANTS = [(0, None, None, None)] + [(5, *sh.split(":")) for sh in a.shapes.split(",")]
@@ -47,6 +60,9 @@ def main():
         kind, arg = CONFIGS[name]()
         if kind == "poisson":
             m = cga.Matrix.poisson(q, *arg)
+        elif kind == "g3":
+            rp, cl, vl = workloads.host_csr("g3_standin")
+            m = cga.Matrix(q, vl, cl, rp)
         else:
             rp, cl, vl = workloads.irregular_spd(arg)
             m = cga.Matrix(q, vl, cl, rp)
@@ -56,9 +72,16 @@ def main():
         res = {}
         for rnd in range(a.rounds):
             for mode, R, tg, nt in VARIANTS:
+                for k, v in base_env.items():
+                    if R:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
                 if R:
-                    os.environ["CGX_COOP_R"] = R
-                    os.environ["CGX_COOP_TAGR"] = tg
+                    if R != "0":
+                        os.environ["CGX_COOP_R"] = R
+                    os.environ["CGX_COOP_TAGR"] = "1" if tg == "1" else "0"
+                    os.environ["CGX_COOP_STREAM"] = "1" if tg == "2" else "0"
                     os.environ["CGX_COOP_NT"] = nt
                 x = torch.zeros(n, dtype=torch.float64, device="cuda")
                 torch.cuda.synchronize()
@@ -82,12 +105,13 @@ def main():
                 rxr = C.c_double()
                 check(L.cgx_cg_rxr(cg, C.byref(rxr)))
                 check(L.cgx_cg_destroy(cg))
-                key = (mode if mode != 5 else f"5/R{R}/tagr{tg}/nt{nt}")
+                key = (mode if mode != 5 else f"5/R{R}/form{tg}/nt{nt}")
                 ran = bodies.value - a.warmup
                 res.setdefault(key, []).append((dt / max(ran, 1) * 1e6, ran, me.value, rxr.value))
                 os.environ.pop("CGX_COOP_R", None)
                 os.environ.pop("CGX_COOP_TAGR", None)
                 os.environ.pop("CGX_COOP_NT", None)
+                os.environ.pop("CGX_COOP_STREAM", None)
         for k, v in res.items():
             us = sorted(t[0] for t in v)
             print(json.dumps({"config": name, "n": n, "mode": k, "mode_eff": v[0][2], "bodies": v[0][1],
