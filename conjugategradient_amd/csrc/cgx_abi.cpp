@@ -405,6 +405,13 @@ int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
   });
 }
 
+// $CGX_COOP_REG_MAXG: workgroups of mode 5's register forms (A/B; default
+// kCoopMaxGReg)
+int coop_reg_maxg() {
+  const char *e = std::getenv("CGX_COOP_REG_MAXG");
+  return e ? std::max(1, std::atoi(e)) : kCoopMaxGReg;
+}
+
 // $CGX_COOP_R: mode 5's rows per thread (1, 2, 4; unset: the fewest that fit)
 int coop_want_r() {
   const char *e = std::getenv("CGX_COOP_R");
@@ -2074,7 +2081,7 @@ static bool coop_auto(const cgx_cg *cg) {
   }
   // rows whose entries all sit in registers (7 in the 1,024-thread form)
   const int kc = cg->coop_nt == 1024 ? 7 : kCoopK;
-  return A->max_row_nnz <= kc && coop_rows_per_thread(cg->n, 1, cg->coop_nt) == 1 &&
+  return A->max_row_nnz <= kc && coop_rows_per_thread(cg->n, 1, cg->coop_nt, coop_reg_maxg()) == 1 &&
          coop_fits(cg, 1);
 }
 
@@ -2100,8 +2107,16 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   if (mode == 5) {
     CGX_REQUIRE(!cg->A->dist && cg->dtype == CGX_F64, CGX_EUNSUPPORTED,
                 "mode 5 (persistent body) runs f64 on a single device");
-    if (cg->coop_stream_want != 1) {
-      coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
+    // rows past the register entries (7 in the 1,024-thread form) read their
+    // tails per thread from the CSR arrays in the register forms: the
+    // streamed form is faster there (irregular 100k rows: 11.2 against 15.0
+    // us per body, profiles/r03_coop_stream*.log) and is taken when it fits
+    const int kc = cg->coop_nt == 1024 ? 7 : kCoopK;
+    const bool prefer_stream =
+        cg->coop_stream_want == 1 ||
+        (cg->coop_stream_want != 0 && cg->A->max_row_nnz > kc && coop_stream_r(cg) > 0);
+    if (!prefer_stream) {
+      coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt, coop_reg_maxg());
       if (coop_r > 0 && !coop_fits(cg, coop_r)) coop_r = 0;
     }
     if (coop_r == 0 && cg->coop_stream_want != 0) {
@@ -2125,7 +2140,7 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
   if (mode == 0) {
     mode = coop_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
-    if (mode == 5) coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt);
+    if (mode == 5) coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt, coop_reg_maxg());
     if (mode != 5 || coop_r == 0) {
       mode = coop_stream_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
       if (mode == 5) {

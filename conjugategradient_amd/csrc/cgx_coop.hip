@@ -692,14 +692,14 @@ __global__ __launch_bounds__(1024, 1) void k_cg_coop_st(
 
 }  // namespace
 
-int coop_rows_per_thread(int64_t n, int want, int nt) {
+int coop_rows_per_thread(int64_t n, int want, int nt, int max_g) {
   static const int opts[] = {1, 2, 4};
   if (nt != 256 && nt != 512 && nt != 1024) return 0;
   for (int R : opts) {
     if (want > 0 && R != want) continue;
     if (nt == 1024 && R != 1) continue;  // 128 VGPRs at 16 waves per CU
     if (nt == 512 && R > 2) continue;    // <4, 512> spills
-    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= kCoopMaxGReg) return R;
+    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= std::min(max_g, kCoopMaxG)) return R;
   }
   return 0;
 }
@@ -721,7 +721,7 @@ hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const 
   const bool tagged = form == 1;
   if (G < 1 || G > kCoopMaxG || m < 1 || (tagged && !g)) return hipErrorInvalidValue;
   if (form == 2 && (NT != 1024 || R < 1 || R > kCoopStreamMaxR)) return hipErrorInvalidValue;
-  if (form != 2 && G > kCoopMaxGReg) return hipErrorInvalidValue;
+
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
   if (e == hipSuccess && tagged) e = hipMemsetAsync(g, 0, (size_t)n * 48, s);
   if (e != hipSuccess) return e;

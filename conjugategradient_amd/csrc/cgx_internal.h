@@ -294,7 +294,9 @@ enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 // ---- persistent CG body (mode 5, cgx_coop.hip) -------------------------------
 constexpr int kCoopK = 8;       // entries per row held in registers
 constexpr int kCoopMaxG = 256;     // workgroups: at most one per CU (exchange granules)
-constexpr int kCoopMaxGReg = 128;  // the register forms: at most one per CU on half the chip
+// the register forms' default cap ($CGX_COOP_REG_MAXG); the device's CU
+// count bounds every form (one workgroup per CU)
+constexpr int kCoopMaxGReg = 256;
 // exchange granules ({tag, half of a double}: two per workgroup and exchange),
 // zeroed before every launch
 struct CoopWs {
@@ -306,7 +308,7 @@ struct CoopWs {
 // rows per thread (1, 2 or 4; `want` > 0 asks for one) for which n rows fit
 // kCoopMaxGReg workgroups of nt threads (256, or 1024 with one row per
 // thread); 0: none
-int coop_rows_per_thread(int64_t n, int want, int nt);
+int coop_rows_per_thread(int64_t n, int want, int nt, int max_g = kCoopMaxGReg);
 // the streamed form (2): the least R <= kCoopStreamMaxR for which n rows fit
 // min(max_g, kCoopMaxG) workgroups of 1,024 threads; 0: none
 constexpr int kCoopStreamMaxR = 8;

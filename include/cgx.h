@@ -187,7 +187,7 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * beta p_{k-1} computed where the SpMV reads it and stored once into the
  * p ring, update_r with the stop rule, x from the four p buffers in slot 3
  * (72 N + matrix bytes per body against 78 N in mode 3); 5 persistent body
- * (single device, f64; register forms up to 131072 rows, the streamed form
+ * (single device, f64; register forms up to 1024 rows per CU, the streamed form
  * up to 8 x 1024 x min(256, CUs) rows): one launch runs a whole chunk of
  * bodies, each with two grid-wide exchanges of the dot partials instead of
  * three kernel boundaries; Ap bit-identical, the dots summed in another

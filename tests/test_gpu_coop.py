@@ -150,12 +150,29 @@ def test_mode5_solves_to_tolerance_and_warm_start(queue, oracle):
     assert abs(it5 - res.iterations) <= 2 and rel(x5, xr) <= 1e-10
 
 
-def test_mode5_irregular_rows(queue, oracle):
+def test_mode5_register_form_on_256_workgroups(queue, oracle):
+    """512^2 (262,144 rows): the register form on 256 workgroups of 1,024
+    threads, one per CU (the exchange sweep reads four partials per lane)."""
+    rp, cl, vl = oracle.poisson(2, 512, 512, 1)
+    n = len(rp) - 1
+    m = cga.Matrix(queue, vl, cl, rp)
+    b = np.arange(1, n + 1, dtype=np.float64)
+    shape = []
+    x5, it5, r5 = _solve(queue, m, b, 5, 0.0, max_iter=40, shape=shape)
+    assert shape[0] == (1, 1024, 256, 0)
+    x1, it1, r1 = _solve(queue, m, b, 1, 0.0, max_iter=40)
+    assert it5 == it1 == 40
+    assert rel(x5, x1) <= 1e-11 and r5 == pytest.approx(r1, rel=1e-9)
+
+
+@pytest.mark.parametrize("stream", ["0", "1"], ids=["register", "streamed"])
+def test_mode5_irregular_rows(queue, oracle, monkeypatch, stream):
     """Rows longer than the kCoopK entries held in registers (a hub row of
     300 entries) read their tail from the CSR arrays. Diagonal shift 10: a
     well-conditioned system, where 30 bodies in two summation orders agree to
     1e-15 on the CPU (with the stand-in's shift of 1e-2 the oracle's own 1-
     and 8-thread runs differ by 5e-3 after 30 bodies on this hub matrix)."""
+    monkeypatch.setenv("CGX_COOP_STREAM", stream)
     rp, cl, vl = irregular_spd(20000, seed=4, hub=300, shift=10.0)
     assert np.diff(rp).max() > 8
     m = cga.Matrix(queue, vl, cl, rp)
@@ -200,14 +217,15 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
     finally:
         L.cgx_cg_destroy(h)
     del big
-    # past the register forms: the streamed form; in auto only on the
-    # CSR-stream path at <= 2 rows per thread (an irregular 200k-row matrix,
-    # not a 3-D stencil of 163,840 rows, not 1,000,000 rows)
+    # which form: a 3-D stencil of 163,840 rows (160 workgroups) keeps its
+    # entries in registers, also in auto; an irregular 200k-row matrix (rows
+    # past 7 entries) takes the streamed form, also in auto (CSR-stream path,
+    # one row per thread); 1,000,000 rows: the streamed form only when asked
     rp, cl, vl = irregular_spd(200000, seed=5)
-    cases = ((lambda: cga.Matrix(queue, vl, cl, rp), True),
-             (lambda: cga.Matrix.poisson(queue, 3, 64, 64, 40), False),
-             (lambda: cga.Matrix.poisson(queue, 3, 100, 100, 100), False))
-    for make, auto5 in cases:
+    cases = ((lambda: cga.Matrix.poisson(queue, 3, 64, 64, 40), True, 0),
+             (lambda: cga.Matrix(queue, vl, cl, rp), True, 2),
+             (lambda: cga.Matrix.poisson(queue, 3, 100, 100, 100), False, 2))
+    for make, auto5, form in cases:
         mid = make()
         check(L.cgx_cg_create(queue.handle, mid.schedule(), C.byref(h)))
         try:
@@ -216,7 +234,7 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
             check(L.cgx_cg_get_mode(h, C.byref(mode)))
             assert (mode.value == 5) == auto5
             check(L.cgx_cg_set_mode(h, 5))
-            assert _shape(h)[3] == 2
+            assert _shape(h)[3] == form
         finally:
             L.cgx_cg_destroy(h)
 

@@ -31,6 +31,8 @@ CONFIGS = {
     "p3d_80": lambda: ("poisson", (3, 80, 80, 80)),
     "p2d_700": lambda: ("poisson", (2, 700, 700, 1)),
     "irr_200k": lambda: ("irr", 200000),
+    "p3d_60": lambda: ("poisson", (3, 60, 60, 60)),
+    "p2d_400": lambda: ("poisson", (2, 400, 400, 1)),
     "g3": lambda: ("g3", None),
 }
 
