@@ -508,6 +508,14 @@ int build_graph(cgx_cg *cg, int slot0, int64_t iters, hipGraphExec_t *out) {
   e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   CGX_HIP(e);
+#ifndef CGX_NO_GRAPH_UPLOAD
+  // the executable graph's packets onto the device now, not at its first
+  // launch (cgx_cg_prepare: out of a timed region)
+  if ((e = hipGraphUpload(ge, s)) != hipSuccess) {
+    (void)hipGraphExecDestroy(ge);
+    CGX_HIP(e);
+  }
+#endif
   cg->graph_x = cg->x;
   cg->graphs[{slot0, iters}] = ge;
   *out = ge;
