@@ -1252,23 +1252,35 @@ extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, i
 // one chunk, and the p rows they gather (~1.3 MB at 256^3) stay in the
 // XCD's 4 MB L2, where plane-by-plane order spans two whole planes and
 // re-fetches p. Empty when planes are small (< 256 slices).
-static std::vector<int> sell_visit_order(int64_t nsl, int64_t H, int64_t P) {
-  constexpr int64_t kChunk = 128;
+// The same order over a list of slice ids (ascending; a partitioned matrix's
+// interior slices, cgx_dist.cpp): positions are split into eighths as the
+// kernel's sell_range splits a list. Empty when no reordering applies.
+std::vector<int> chunked_slice_order(const std::vector<int> &ids, int64_t H, int64_t P,
+                                     int64_t kChunk) {
+  if (const char *env = std::getenv("CGX_SELL_ORDER_CHUNK"))  // A/B knob
+    kChunk = std::max<int64_t>(1, std::atoll(env));
   std::vector<int> order;
   if (P / H < 2 * kChunk) return order;
-  order.resize((size_t)nsl);
+  const int64_t m = (int64_t)ids.size();
+  order.resize((size_t)m);
   std::vector<std::tuple<int64_t, int64_t, int64_t, int>> key;
   for (int g = 0; g < 8; ++g) {
-    const int64_t lo = (nsl * g) >> 3, hi = (nsl * (g + 1)) >> 3;
+    const int64_t lo = (m * g) >> 3, hi = (m * (g + 1)) >> 3;
     key.clear();
-    for (int64_t q = lo; q < hi; ++q) {
-      const int64_t r0 = q * H, z = r0 / P, u = (r0 % P) / H;
-      key.emplace_back(u / kChunk, z, u, (int)q);
+    for (int64_t i = lo; i < hi; ++i) {
+      const int q = ids[(size_t)i];
+      const int64_t r0 = (int64_t)q * H, z = r0 / P, u = (r0 % P) / H;
+      key.emplace_back(u / kChunk, z, u, q);
     }
     std::sort(key.begin(), key.end());
-    for (size_t i = 0; i < key.size(); ++i) order[(size_t)lo + i] = std::get<3>(key[i]);
+    for (size_t k = 0; k < key.size(); ++k) order[(size_t)lo + k] = std::get<3>(key[k]);
   }
   return order;
+}
+static std::vector<int> sell_visit_order(int64_t nsl, int64_t H, int64_t P, int64_t kChunk) {
+  std::vector<int> ids((size_t)nsl);
+  for (int64_t q = 0; q < nsl; ++q) ids[(size_t)q] = (int)q;
+  return chunked_slice_order(ids, H, P, kChunk);
 }
 
 // Value codes of A's SELL-P copy (cgx_internal.h kVcMax): the
@@ -1530,14 +1542,23 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
     free_sell(A);
     return hip_fail(e, "cgx_csr_create(SELL copy)");
   }
-  // visit order, opt-in ($CGX_SELL_ORDER=1): it measured no faster at 256^3
-  // (the re-fetched p lines are Infinity-Cache hits)
+  // visit order: automatic for single-device matrices whose planes span at
+  // least two chunks of 512 slices (the XCD's ~1,024 slices in flight then
+  // hold every +-plane gather in its L2: 512^3 SpMV 793 -> 710 us, the
+  // iteration 463 -> 483 it/s; profiles/r03m_order_chunk.log). 256^3
+  // planes (512 slices) keep the natural order, which is the same walk.
+  // $CGX_SELL_ORDER=1 forces it with chunks of 128 slices (the round-2
+  // form, no faster at 256^3: DESIGN.md §8), =0 turns it off.
   {
     int64_t P = 0;
     for (int v : pool) P = std::max<int64_t>(P, v < 0 ? -(int64_t)v : v);
     const char *env = std::getenv("CGX_SELL_ORDER");
+    const int req = env ? std::atoi(env) : -1;
     std::vector<int> order;
-    if (env && std::atoi(env) == 1) order = sell_visit_order(nsl, (int64_t)kSellRows * R, P);
+    if (req == 1)
+      order = sell_visit_order(nsl, (int64_t)kSellRows * R, P, 128);
+    else if (req < 0 && !A->dist)
+      order = sell_visit_order(nsl, (int64_t)kSellRows * R, P, 512);
     if (!order.empty()) {
       e = hipMalloc(&A->d_sell_order, order.size() * sizeof(int));
       if (e == hipSuccess)

@@ -175,3 +175,39 @@ def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
     xr, res = oracle.cg_solve(rp, cl, vl, b, 1e-8)
     assert abs(cg.iterations - res.iterations) <= 2
     assert rel(cg.extract(), xr) <= 1e-10
+
+
+def test_auto_visit_order_on_large_planes(queue, oracle, monkeypatch):
+    """Planes of >= 1,024 slices get the chunked visit order without any
+    request (cgx_abi.cpp build_sell; 512^3: SpMV 793 -> 710 us): the SpMV
+    stays bit-exact against the oracle in the production form and in
+    CSR-stream, and CG holds the oracle's iterates (only the p.Ap partials'
+    grouping changes)."""
+    monkeypatch.delenv("CGX_SELL_ORDER", raising=False)
+    monkeypatch.delenv("CGX_SELL_ORDER_CHUNK", raising=False)
+    rp, cl, vl = oracle.poisson(3, 512, 256, 4)  # planes of 131,072 rows = 1,024 slices
+    n = len(rp) - 1
+    A = Matrix(queue, vl, cl, rp)
+    v = C.c_int()
+    check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
+    prod = v.value
+    assert prod & 8192, prod  # SELL-P (the ordered walk)
+    x = np.random.default_rng(11).standard_normal(n)
+    ref = oracle.spmv(rp, cl, vl, x)
+    ops = VectorOperations(queue)
+    ops.setVectorSize(n)
+    xv = Vector(queue, x)
+    for var in (prod, 15):
+        check(lib().cgx_csr_set_variant(A.schedule(), var))
+        yv = Vector(queue, n)
+        ops.spmv(A, xv, yv, A.NNZ(), count=n)
+        np.testing.assert_array_equal(yv.to_numpy(), ref, err_msg=f"variant {var}")
+    check(lib().cgx_csr_set_variant(A.schedule(), prod))
+    b = np.arange(1, n + 1, dtype=np.float64)
+    cg = cga.CG(queue)
+    cg.setMatrix(A)
+    cg.setTarget(b)
+    cg.solve(0.0, max_iter=30)
+    xr, res = oracle.cg_solve(rp, cl, vl, b, 0.0, max_iter=30)
+    assert cg.iterations == res.iterations
+    assert rel(cg.extract(), xr) <= 1e-12
