@@ -2372,6 +2372,7 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   long long last_bodies = -1;
   int last_stopped = 0;
   long long bodies_before = -1;
+  bool flushed = false;
   auto wait_one = [&]() -> int {
     Pending pd = q.front();
     q.erase(q.begin());
@@ -2414,6 +2415,13 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
       if ((rc = poll_state(cg, hbuf + 256 * buf, s))) break;
       CGX_HIP(hipEventRecord(ev[buf], s));
       q.push_back(Pending{buf, cg->slot, chunk});
+      if (remaining == 0 && !cg->A->dist && !cg->coop) {
+        // the end-of-run x flush reads only device state and the slot, so a
+        // single-device run queues it behind its last chunk instead of after
+        // the host has seen that chunk finish (one host round trip less)
+        if ((rc = flush_pending_x(cg))) break;
+        flushed = true;
+      }
       continue;
     }
     if ((rc = wait_one())) break;
@@ -2433,7 +2441,7 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
               "the launch was not resident); the solve was stopped, x is not updated");
     return CGX_EHIP;
   }
-  if ((rc = flush_pending_x(cg))) return rc;
+  if (!flushed && (rc = flush_pending_x(cg))) return rc;
   CGX_HIP(hipStreamSynchronize(s));
   if (cg->timing) {
     CGX_HIP(hipStreamSynchronize(s));
