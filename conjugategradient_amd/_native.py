@@ -65,6 +65,7 @@ _SIGS = {
     "cgx_csr_set_sell": (_i32, [_vp, _i32]),
     "cgx_csr_split_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     "cgx_csr_sell_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(C.c_int64)]),
+    "cgx_csr_visit_order": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_value_codes": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_templates": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i64)]),
     "cgx_csr_march_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),

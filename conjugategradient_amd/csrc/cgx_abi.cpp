@@ -1665,6 +1665,12 @@ extern "C" int cgx_csr_march_info(cgx_csr *A, int *stride, int *offset_a, int *r
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_visit_order(cgx_csr *A, int *ordered) {
+  CGX_REQUIRE(A && ordered, CGX_EINVAL, "NULL argument");
+  *ordered = A->dev.sorder ? 1 : (A->split_ni > 0 && A->split_ordered) ? 2 : 0;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
   if (has_sell) *has_sell = !A->dev.sl ? 0 : (A->dev.sell_kind ? 3 : A->dev.sell_r);

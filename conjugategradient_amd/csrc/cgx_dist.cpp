@@ -640,7 +640,10 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
           if (c < n_local) P = std::max<int64_t>(P, c > r ? c - r : r - c);
         }
       std::vector<int> o = chunked_slice_order(in, H, P, oreq == 1 ? 128 : 512);
-      if (!o.empty()) in.swap(o);
+      if (!o.empty()) {
+        in.swap(o);
+        A->split_ordered = true;
+      }
     }
     if (!in.empty() && !bd.empty()) {
       in.insert(in.end(), bd.begin(), bd.end());

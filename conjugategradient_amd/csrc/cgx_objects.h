@@ -165,6 +165,7 @@ struct cgx_csr {
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;
   int split_ni = 0, split_nb = 0;
+  bool split_ordered = false;  // interior list in the chunked visit order
   hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
   cgx::Peer peer;  // device peer transport (cgx_dist_peer_enable)
   int64_t sell_padded = 0;

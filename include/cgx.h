@@ -97,6 +97,11 @@ int cgx_csr_set_sell(cgx_csr *csr, int rows_per_lane);
 /* The matrix's SELL layout (0 none, 1 / 2 dictionary SELL with that many
  * rows per lane, 3 SELL-P) and its padded entry count. */
 int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
+/* The SELL walk's slice visit order: 1 when the slices are walked in
+ * XCD-local chunks of z-planes (automatic where planes span >= 1,024
+ * slices; $CGX_SELL_ORDER), 2 when a partitioned matrix's interior slice
+ * list is, 0 for the natural order. */
+int cgx_csr_visit_order(cgx_csr *csr, int *ordered);
 /* Distinct values of the matrix's SELL-P value codes (variant bit 32768:
  * one code byte per slot into a dictionary of at most 255 values, built by
  * cgx_csr_create when the SELL-P copy exists and the matrix has that few

@@ -192,6 +192,9 @@ def test_auto_visit_order_on_large_planes(queue, oracle, monkeypatch):
     check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
     prod = v.value
     assert prod & 8192, prod  # SELL-P (the ordered walk)
+    o = C.c_int(-1)
+    check(lib().cgx_csr_visit_order(A.schedule(), C.byref(o)))
+    assert o.value == 1
     x = np.random.default_rng(11).standard_normal(n)
     ref = oracle.spmv(rp, cl, vl, x)
     ops = VectorOperations(queue)
