@@ -54,6 +54,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+KVL = 33554432  # variant bit of the lean stencil walk (include/cgx.h cgx_csr_lean_info)
 METRIC = "CG iterations/sec + achieved HBM GB/s, 256³ 7-pt Poisson fp64, 1/2/4/8 GPUs"
 
 
@@ -359,6 +360,9 @@ def run(args) -> None:
     check(L.cgx_csr_stream_bytes(A, C.byref(sbytes)))
     ntpl, tpl_slices = C.c_int(0), C.c_int64(0)
     check(L.cgx_csr_templates(A, C.byref(ntpl), C.byref(tpl_slices)))
+    lean = [C.c_int(0), C.c_int64(0), C.c_int(0), C.c_int(0), C.c_int(0)]
+    check(L.cgx_csr_lean_info(A, *[C.byref(v) for v in lean]))
+    lean_on = bool(variant.value & KVL)
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
@@ -431,7 +435,8 @@ def run(args) -> None:
         ach = kb / (avg[1] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
             (16 * n_local if mode_eff == 4 else 0)
-        kname = {2: "k_spmv_fused", 4: "k_spmv_fd"}.get(mode_eff, "k_spmv_dot")
+        kname = {2: "k_spmv_fused", 4: "k_spmv_fd"}.get(
+            mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname,
@@ -450,10 +455,13 @@ def run(args) -> None:
         if world == 1 and not args.no_traffic:
             # HBM bytes per launch from rocprofv3 PMC passes of this same
             # workload, variant and mode (child processes, after this run)
-            t = pmc_traffic(args, int(variant.value), mode_eff)
+            # (a lean walk is forced at the grid its class layout was built for)
+            t = pmc_traffic(args, f"{int(variant.value)}:{lean[2].value}" if lean_on
+                            else str(int(variant.value)), mode_eff)
             roof["traffic_by_kernel"] = t.get("by_kernel")
             roof["traffic_method"] = t.get("method")
-            key = f"{kname}<double, {int(variant.value)}>"
+            key = (f"{kname}<double>" if kname == "k_spmv_lean"
+                   else f"{kname}<double, {int(variant.value & ~KVL)}>")
             if t.get("by_kernel") and key in t["by_kernel"]:
                 roof["traffic"] = t["by_kernel"][key]
                 roof["traffic_ratio_to_compulsory"] = round(roof["traffic"] / kb, 4)
@@ -519,7 +527,12 @@ def run(args) -> None:
                            {"templates": ntpl.value, "slices": tpl_slices.value,
                             "slices_total": (n_local + 127) // 128,
                             "in_use": bool(variant.value & 8388608)}
-                           if ntpl.value else None)},
+                           if ntpl.value else None),
+                       "lean_walk": (
+                           {"classes": lean[0].value, "slices": lean[1].value,
+                            "slices_total": (n_local + 127) // 128, "grid": lean[2].value,
+                            "D": lean[3].value, "a": lean[4].value, "in_use": lean_on}
+                           if lean[0].value else None)},
             "roofline": roof,
             "csr_general": general,
             "cpu_baseline": cpu,
@@ -589,7 +602,7 @@ def pmc_bytes(sums: dict) -> dict:
     return out
 
 
-def pmc_traffic(args, variant: int, mode: int, timeout_s: float = 180.0) -> dict:
+def pmc_traffic(args, variant: str, mode: int, timeout_s: float = 180.0) -> dict:
     """HBM bytes per launch of every kernel of the iteration, from two
     rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE: one counter group per
     run, kernel dispatch counters only) of a short child run of this same
@@ -611,7 +624,7 @@ def pmc_traffic(args, variant: int, mode: int, timeout_s: float = 180.0) -> dict
              "--no-general", "--no-traffic", "--mode", str(mode), "--poll", str(args.poll)]
     if args.grid:
         child += ["--grid", str(args.grid)]
-    env = dict(os.environ, CGX_SPMV_VARIANT=str(variant))
+    env = dict(os.environ, CGX_SPMV_VARIANT=variant)
     env.pop("WORLD_SIZE", None)
     sums: dict = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):

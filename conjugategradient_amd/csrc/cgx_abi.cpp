@@ -483,7 +483,11 @@ int flush_pending_x(cgx_cg *cg) {
   return CGX_OK;
 }
 
+// A cached exec may still be in flight (cgx_cg_run keeps two chunks queued):
+// the stream drains before any is destroyed.
 void drop_graph(cgx_cg *cg) {
+  if (cg->graphs.empty()) return;
+  (void)hipStreamSynchronize(cg->ctx->stream);
   for (auto &kv : cg->graphs) (void)hipGraphExecDestroy(kv.second);
   cg->graphs.clear();
 }
@@ -508,14 +512,12 @@ int build_graph(cgx_cg *cg, int slot0, int64_t iters, hipGraphExec_t *out) {
   e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   CGX_HIP(e);
-#ifndef CGX_NO_GRAPH_UPLOAD
   // the executable graph's packets onto the device now, not at its first
   // launch (cgx_cg_prepare: out of a timed region)
   if ((e = hipGraphUpload(ge, s)) != hipSuccess) {
     (void)hipGraphExecDestroy(ge);
     CGX_HIP(e);
   }
-#endif
   cg->graph_x = cg->x;
   cg->graphs[{slot0, iters}] = ge;
   *out = ge;
@@ -968,7 +970,22 @@ extern "C" int cgx_csr_info(cgx_csr *A, int64_t *n, int64_t *nnz, int64_t *rbs, 
   return CGX_OK;
 }
 
+void free_lean(cgx_csr *A) {
+  for (void **p : {&A->d_vl_cls, &A->d_vl_tab}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  A->dev.vl_cls = nullptr;
+  A->dev.vl_tab = nullptr;
+  A->dev.vl_grid = A->dev.vl_nst = A->dev.vl_D = A->dev.vl_a = 0;
+  A->dev.lean = false;
+  A->vl_slice_cls.clear();
+  A->vl_ncls = 0;
+}
+
 void free_sell(cgx_csr *A) {
+  free_lean(A);
+  A->sell_pool.clear();
   for (void **p : {&A->d_sell_sl, &A->d_sell_dict, &A->d_sell_idx, &A->d_sell_val,
                    &A->d_sell_order, (void **)&A->d_split, &A->d_sell_mask, &A->d_sell_vc,
                    &A->d_sell_vdict, &A->d_sell_vc4, &A->d_sell_sl_t, &A->d_vct}) {
@@ -1459,6 +1476,236 @@ static int build_value_templates(cgx_csr *A) {
   return CGX_OK;
 }
 
+// Lean stencil walk (cgx_internal.h kVL): the class of every
+// template slice whose pattern is a subset of the stencil's {-D, -a, -1, 0,
+// +1, +a, +D} and whose template chunk holds one value per slot for every row
+// (absent only at the x-line ends' -1 of lane 0 row 0 and +1 of lane 63 row
+// 1, with that slot's value finite), in slice order; the class table; D and
+// a, taken from the most frequent 7-wide (or, 2-D, 5-wide) stencil pattern
+// of the template slices. Host work over the slice table; returns CGX_OK
+// with no classes when the matrix has none. Single-device matrices only.
+static int build_lean_classes(cgx_csr *A, std::vector<VlClass> &tab) {
+  tab.clear();
+  A->vl_slice_cls.clear();
+  const CsrDev &d = A->dev;
+  if (A->dist || !d.sl_t || !d.vct || d.nvt < 1 || !d.svc4 || !d.svdict || d.sell_maxw > 8 ||
+      A->sell_pool.empty() || (uint64_t)(d.n + 2) * dtype_size(A->dtype) >= (uint64_t(1) << 32))
+    return CGX_OK;
+  hipStream_t s = A->ctx->stream;
+  const int64_t nsl = d.nsl;
+  std::vector<SellSlice> sl((size_t)nsl);
+  std::vector<unsigned long long> chunks((size_t)d.nvt * 64);
+  std::vector<double> vd(kVcDict);
+  std::vector<float> vdf;
+  CGX_HIP(hipMemcpyAsync(sl.data(), d.sl_t, (size_t)nsl * sizeof(SellSlice),
+                         hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipMemcpyAsync(chunks.data(), d.vct, chunks.size() * 8, hipMemcpyDeviceToHost, s));
+  if (A->dtype == CGX_F32) {
+    vdf.resize(kVcDict);
+    CGX_HIP(hipMemcpyAsync(vdf.data(), d.svdict, kVcDict * sizeof(float), hipMemcpyDeviceToHost,
+                           s));
+  } else {
+    CGX_HIP(hipMemcpyAsync(vd.data(), d.svdict, kVcDict * sizeof(double), hipMemcpyDeviceToHost,
+                           s));
+  }
+  CGX_HIP(hipStreamSynchronize(s));
+  if (!vdf.empty())
+    for (int k = 0; k < kVcDict; ++k) vd[k] = (double)vdf[k];
+  const std::vector<int> &pool = A->sell_pool;
+  auto offs = [&](const SellSlice &m, int j) { return pool[(size_t)m.dict + j]; };
+  // the stencil: (D, a) of the most frequent full pattern among template slices
+  std::map<std::pair<int, int>, int64_t> freq;
+  for (const SellSlice &m : sl) {
+    const int W = m.width & kVtWidthMask;
+    if ((m.width >> 16) == 0) continue;
+    if (W == 7 && offs(m, 2) == -1 && offs(m, 3) == 0 && offs(m, 4) == 1 &&
+        offs(m, 1) == -offs(m, 5) && offs(m, 0) == -offs(m, 6) && offs(m, 5) > 1 &&
+        offs(m, 6) > offs(m, 5))
+      ++freq[{offs(m, 6), offs(m, 5)}];
+    else if (W == 5 && offs(m, 1) == -1 && offs(m, 2) == 0 && offs(m, 3) == 1 &&
+             offs(m, 0) == -offs(m, 4) && offs(m, 4) > 1)
+      ++freq[{offs(m, 4), 0}];
+  }
+  if (freq.empty()) return CGX_OK;
+  auto best = freq.begin();
+  for (auto it = freq.begin(); it != freq.end(); ++it)
+    if (it->second > best->second) best = it;
+  const int D = best->first.first, a = best->first.second;
+  // canonical slot of offset o (-1: none)
+  auto canon = [&](int o) {
+    if (o == -D) return 0;
+    if (a > 0 && o == -a) return 1;
+    if (o == -1) return 2;
+    if (o == 0) return 3;
+    if (o == 1) return 4;
+    if (a > 0 && o == a) return 5;
+    if (o == D) return 6;
+    return -1;
+  };
+  // the class of (template t, pattern at pool base pb of width W), or -1
+  auto make = [&](int t, int pb, int W, VlClass &c) -> bool {
+    std::memset(&c, 0, sizeof(c));
+    int slot_of[8];
+    bool seen[7] = {};
+    for (int j = 0; j < W; ++j) {
+      const int q = canon(pool[(size_t)pb + j]);
+      if (q < 0 || seen[q]) return false;
+      seen[q] = true;
+      slot_of[j] = q;
+    }
+    if (!seen[2] || !seen[3] || !seen[4]) return false;
+    const unsigned long long *w = chunks.data() + (size_t)t * 64;
+    auto code = [&](int l, int j, int r) { return (unsigned)(w[l] >> (8 * j + 4 * r)) & 0xfu; };
+    for (int j = W; j < 8; ++j)  // slots past the pattern: empty in every row
+      for (int l = 0; l < 64; ++l)
+        if (code(l, j, 0) != 0xfu || code(l, j, 1) != 0xfu) return false;
+    c.plo = c.phi = 1;
+    for (int j = 0; j < W; ++j) {
+      const int q = slot_of[j];
+      int k = -1;
+      for (int r = 0; r < 2; ++r)
+        for (int l = 0; l < 64; ++l) {
+          const unsigned cd = code(l, j, r);
+          if (cd == 0xfu) {
+            if (q == 2 && r == 0 && l == 0) {
+              c.plo = 0;
+              continue;
+            }
+            if (q == 4 && r == 1 && l == 63) {
+              c.phi = 0;
+              continue;
+            }
+            return false;
+          }
+          if (k < 0) k = (int)cd;
+          else if ((int)cd != k) return false;  // codes are distinct bit patterns
+        }
+      if (k < 0) return false;
+      c.v[q] = vd[k];
+      if (q == 0) c.pres |= 1;
+      if (q == 1) c.pres |= 2;
+      if (q == 5) c.pres |= 4;
+      if (q == 6) c.pres |= 8;
+    }
+    if ((!c.plo && !std::isfinite(c.v[2])) || (!c.phi && !std::isfinite(c.v[4]))) return false;
+    c.zlo = -std::copysign(0.0, c.v[2]);
+    c.zhi = -std::copysign(0.0, c.v[4]);
+    return true;
+  };
+  std::map<std::pair<int, int>, int> ids;  // (template, pool base) -> class (-1: none)
+  A->vl_slice_cls.assign((size_t)nsl, 0xff);
+  int64_t lean = 0;
+  for (int64_t q = 0; q < nsl; ++q) {
+    const SellSlice &m = sl[(size_t)q];
+    const int t = (m.width >> 16) - 1, W = m.width & kVtWidthMask;
+    if (t < 0 || (q + 1) * 2 * kSellRows > d.n) continue;  // a template chunk, a full slice
+    auto it = ids.find({t, m.dict});
+    if (it == ids.end()) {
+      VlClass c;
+      int id = -1;
+      if ((int)tab.size() < kVlMaxCls && make(t, m.dict, W, c)) {
+        id = (int)tab.size();
+        tab.push_back(c);
+      }
+      it = ids.emplace(std::make_pair(t, m.dict), id).first;
+    }
+    if (it->second >= 0) {
+      A->vl_slice_cls[(size_t)q] = (unsigned char)it->second;
+      ++lean;
+    }
+  }
+  if (lean == 0) {
+    tab.clear();
+    A->vl_slice_cls.clear();
+    return CGX_OK;
+  }
+  A->dev.vl_D = D;
+  A->dev.vl_a = a;
+  return CGX_OK;
+}
+
+// The classes in the wave-major layout of a G-workgroup launch (G a multiple
+// of 8: waves of XCD group g walk its eighth of the slices with step G / 2)
+// and the table, on the device; the lean walk is then available at grid G.
+static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G) {
+  if (A->vl_slice_cls.empty() || tab.empty() || G < 8 || G % 8) return CGX_EINVAL;
+  const int64_t nsl = A->dev.nsl;
+  const int step = G / 2;
+  int64_t nst = 0;
+  for (int g = 0; g < 8; ++g) {
+    const int64_t lo = (nsl * g) >> 3, end = (nsl * (g + 1)) >> 3;
+    nst = std::max<int64_t>(nst, (end - lo + step - 1) / step);
+  }
+  nst = (nst + 3) & ~int64_t(3);
+  // the forward sweep's rows, then the reversed sweep's (slice lo + end - 1 - q)
+  std::vector<unsigned char> h((size_t)(2 * 8 * step * nst), 0xff);
+  for (int rev = 0; rev < 2; ++rev)
+    for (int g = 0; g < 8; ++g) {
+      const int64_t lo = (nsl * g) >> 3, end = (nsl * (g + 1)) >> 3;
+      for (int w = 0; w < step; ++w) {
+        unsigned char *row = h.data() + (size_t)((int64_t)(rev * 8 * step + g * step + w) * nst);
+        int64_t j = 0;
+        for (int64_t q = lo + w; q < end; q += step)
+          row[j++] = A->vl_slice_cls[(size_t)(rev ? lo + end - 1 - q : q)];
+      }
+    }
+  void *dc = nullptr, *dt = nullptr;
+  hipStream_t s = A->ctx->stream;
+  hipError_t e = hipMalloc(&dc, h.size());
+  if (e == hipSuccess) e = hipMalloc(&dt, tab.size() * sizeof(VlClass));
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, h.data(), h.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(dt, tab.data(), tab.size() * sizeof(VlClass), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    if (dc) (void)hipFree(dc);
+    if (dt) (void)hipFree(dt);
+    return hip_fail(e, "cgx_csr_create(lean stencil classes)");
+  }
+  for (void *p : {A->d_vl_cls, A->d_vl_tab})
+    if (p) (void)hipFree(p);
+  A->d_vl_cls = dc;
+  A->d_vl_tab = dt;
+  A->dev.vl_cls = (const unsigned char *)dc;
+  A->dev.vl_tab = (const VlClass *)dt;
+  A->dev.vl_grid = G;
+  A->dev.vl_nst = (int)nst;
+  A->vl_ncls = (int)tab.size();
+  return CGX_OK;
+}
+
+// The lean walk's grid candidates: G / 2 waves per XCD step; with the step
+// a plane's slices K = D / 128 (or K / 2, K / 4 ...) the +-D gathers are the
+// wave's own centers one (two, four) steps away. Capped by the resident
+// workgroups; the largest resident grid is always a candidate.
+static std::vector<int> lean_grids(const cgx_csr *A) {
+  const int res = A->dtype == CGX_F32 ? Launch<float>::lean_resident()
+                                      : Launch<double>::lean_resident();
+  const int cap = std::max(8, std::min(res, kMaxGrid) / 8 * 8);
+  std::vector<int> gs{cap};
+  const int D = A->dev.vl_D;
+  if (D > 0 && D % (2 * kSellRows) == 0) {
+    int G = 2 * (D / (2 * kSellRows));
+    while (G > cap && G % 16 == 0) G /= 2;
+    // first (the default of a request) when it keeps at least half the chip
+    if (G <= cap && G >= 64 && G % 8 == 0 && G != cap)
+      gs.insert(2 * G >= cap ? gs.begin() : gs.end(), G);
+  }
+  return gs;
+}
+
+// build the lean walk's classes and, at grid G (0: the first candidate), its
+// device layout; false when the matrix has no lean slices
+static bool build_lean(cgx_csr *A, int G = 0) {
+  std::vector<VlClass> tab;
+  if (build_lean_classes(A, tab) != CGX_OK || tab.empty()) return false;
+  if (G == 0) G = lean_grids(A).front();
+  return build_lean_layout(A, tab, G) == CGX_OK;
+}
+// the variant under the lean walk: its generic slices' form (4-bit value
+// codes on templates, the pipelined stencil walk's requirements)
+constexpr int kVlBase = 2050 | 32768 | 262144 | 524288 | 1048576 | kVT;
+
 int build_value_codes(cgx_csr *A) {
   if (!A->dev.sl || !A->dev.sell_kind || A->dev.nsl < 1 || A->dev.nnz < 1) return CGX_OK;
   const int rc =
@@ -1574,6 +1821,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   }
   A->dev.sl = (const SellSlice *)A->d_sell_sl;
   A->dev.sdict = (const int *)A->d_sell_dict;
+  A->sell_pool = pool;
   A->dev.sidx = (const unsigned long long *)A->d_sell_idx;
   A->dev.sval = A->d_sell_val;
   A->dev.nsl = nsl;
@@ -1630,7 +1878,14 @@ extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
   const int v = launch_variant(A->dev, A->dtype);
   const int64_t es = (int64_t)dtype_size(A->dtype), nsl = A->dev.nsl;
   const int64_t desc = nsl * (int64_t)sizeof(SellSlice);
-  if ((v & 32768) && (v & kVT))  // template slices read their chunk from LDS
+  if (v & kVL) {  // one class byte per slice; the per-slice form's slices: descriptor and
+                  // (not templated) chunk
+    int64_t gen = 0;
+    for (unsigned char c : A->vl_slice_cls) gen += c == 0xff;
+    *bytes = 4 * (int64_t)A->dev.vl_grid * A->dev.vl_nst + gen * (int64_t)sizeof(SellSlice) +
+             8 * (A->vc_chunks - 64 * A->vt_slices) + 512 * (int64_t)A->dev.nvt +
+             (int64_t)A->vl_ncls * (int64_t)sizeof(VlClass);
+  } else if ((v & 32768) && (v & kVT))  // template slices read their chunk from LDS
     *bytes = 8 * (A->vc_chunks - 64 * A->vt_slices) + desc + 512 * (int64_t)A->dev.nvt;
   else if (v & 32768)
     *bytes = ((v & 262144) ? 8 : 16) * A->vc_chunks + desc;
@@ -1653,6 +1908,21 @@ extern "C" int cgx_csr_templates(cgx_csr *A, int *n_templates, int64_t *slices) 
   CGX_REQUIRE(A && n_templates && slices, CGX_EINVAL, "NULL argument");
   *n_templates = A->dev.sl_t ? A->dev.nvt : 0;
   *slices = A->dev.sl_t ? A->vt_slices : 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_lean_info(cgx_csr *A, int *classes, int64_t *slices, int *grid, int *D,
+                                 int *a) {
+  CGX_REQUIRE(A && classes && slices && grid && D && a, CGX_EINVAL, "NULL argument");
+  const bool on = A->dev.vl_cls != nullptr;
+  int64_t cnt = 0;
+  if (on)
+    for (unsigned char c : A->vl_slice_cls) cnt += c != 0xff;
+  *classes = on ? A->vl_ncls : 0;
+  *slices = cnt;
+  *grid = on ? A->dev.vl_grid : 0;
+  *D = on ? A->dev.vl_D : 0;
+  *a = on ? A->dev.vl_a : 0;
   return CGX_OK;
 }
 
@@ -1695,6 +1965,25 @@ static bool known_variant(int v) {
 
 extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
   CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  if (variant & kVL) {  // the lean stencil walk (at its first grid candidate unless built)
+    CGX_REQUIRE((variant & ~kVL) == 0 || (variant & ~kVL) == kVlBase ||
+                    (variant & ~kVL) == ((kVlBase & ~2048) | 8192),
+                CGX_EINVAL, "unknown SpMV variant %d (the lean walk is %d)", variant,
+                kVL | kVlBase);
+    CGX_REQUIRE(A->dev.sl_t, CGX_EUNSUPPORTED,
+                "variant %d needs value-code templates, which this matrix does not have",
+                variant);
+    DeviceGuard g(A->ctx->device);
+    if (!A->dev.vl_cls) {
+      CGX_REQUIRE(build_lean(A), CGX_EUNSUPPORTED,
+                  "variant %d: no slice of this matrix qualifies for the lean stencil walk",
+                  variant);
+    }
+    A->dev.variant = kVlBase;
+    A->dev.lean = true;
+    return CGX_OK;
+  }
+  A->dev.lean = false;
   CGX_REQUIRE(known_variant(variant), CGX_EINVAL, "unknown SpMV variant %d", variant);
   CGX_REQUIRE(!(variant & (2048 | 8192)) || A->dev.sl, CGX_EUNSUPPORTED,
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
@@ -1734,12 +2023,22 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
 int autotune_spmv(cgx_csr *A) {
   if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
     // the same checks as cgx_csr_set_variant: a mistyped value fails here,
-    // not later as a kernel launch error
+    // not later as a kernel launch error; "V:G" forces the lean walk's grid
     const int v = std::atoi(env);
+    const char *colon = std::strchr(env, ':');
+    const int G = colon ? std::atoi(colon + 1) : 0;
     if (cgx_csr_set_variant(A, v) != CGX_OK) {
       const std::string why = g_err;
       set_error("$CGX_SPMV_VARIANT=%s: %s", env, why.c_str());
       return CGX_EINVAL;
+    }
+    if ((v & kVL) && G > 0) {
+      std::vector<VlClass> tab;
+      if (build_lean_classes(A, tab) != CGX_OK || tab.empty() ||
+          build_lean_layout(A, tab, G) != CGX_OK) {
+        set_error("$CGX_SPMV_VARIANT=%s: no lean walk at grid %d", env, G);
+        return CGX_EINVAL;
+      }
     }
     if (!(v & (2048 | 8192))) free_sell(A);
     return CGX_OK;
@@ -1881,11 +2180,68 @@ int autotune_spmv(cgx_csr *A) {
     if (ap) (void)hipFree(ap);
     if (e == hipSuccess && tf[1] < tf[0]) best_v = pair[1];
   }
+  // The lean stencil walk (kVL) at each of its grid candidates against the
+  // winner so far, interleaved rounds as above (its generic slices run the
+  // template value-code form, its base variant)
+  std::vector<VlClass> vtab;
+  int lean_G = 0;
+  if (e == hipSuccess && A->dev.sl_t && build_lean_classes(A, vtab) == CGX_OK && !vtab.empty()) {
+    const std::vector<int> gs = lean_grids(A);
+    std::vector<float> tl(gs.size() + 1, 1e30f);  // [0]: the incumbent
+    for (int round = 0; round < 3 && e == hipSuccess; ++round)
+      for (size_t k = 0; k <= gs.size() && e == hipSuccess; ++k) {
+        CsrDev dv = A->dev;
+        dv.variant = best_v;
+        if (k > 0) {
+          if (build_lean_layout(A, vtab, gs[k - 1]) != CGX_OK) {
+            e = hipErrorOutOfMemory;
+            break;
+          }
+          dv = A->dev;
+          dv.variant = kVlBase;
+          dv.lean = true;
+        }
+        float tot = 0;
+        for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
+          if (rep == 1) e = hipEventRecord(e0, s);
+          if (e != hipSuccess) break;
+          if (A->dtype == CGX_F32)
+            e = k ? Launch<float>::spmv_dot(dv, (const float *)x, (float *)y,
+                                            (CgScalars<float> *)st, 0, (RedWs<float> *)ctx->ws, s)
+                  : Launch<float>::spmv_dot_variant(best_v, dv, (const float *)x, (float *)y,
+                                                    (CgScalars<float> *)st,
+                                                    (RedWs<float> *)ctx->ws, s);
+          else
+            e = k ? Launch<double>::spmv_dot(dv, (const double *)x, (double *)y,
+                                             (CgScalars<double> *)st, 0,
+                                             (RedWs<double> *)ctx->ws, s)
+                  : Launch<double>::spmv_dot_variant(best_v, dv, (const double *)x, (double *)y,
+                                                     (CgScalars<double> *)st,
+                                                     (RedWs<double> *)ctx->ws, s);
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, s);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
+        if (e == hipSuccess) tl[k] = std::min(tl[k], tot);
+      }
+    for (size_t k = 1; k <= gs.size() && e == hipSuccess; ++k)
+      if (tl[k] < tl[0] && (lean_G == 0 || tl[k] < tl[(size_t)(std::find(gs.begin(), gs.end(),
+                                                                          lean_G) - gs.begin()) + 1]))
+        lean_G = gs[k - 1];
+  }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   for (void *p : {x, y, st})
     if (p) (void)hipFree(p);
+  if (e != hipSuccess) free_lean(A);
   CGX_HIP(e);
+  if (lean_G > 0) {
+    if (int rc = build_lean_layout(A, vtab, lean_G)) return rc;
+    A->dev.variant = kVlBase;
+    A->dev.lean = true;
+    return CGX_OK;
+  }
+  free_lean(A);
   A->dev.variant = best_v;
   if (!(best_v & (2048 | 8192))) free_sell(A);
   if (!(best_v & kC16) || (best_v & 8192)) free_col16(A);
@@ -2192,7 +2548,6 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   if (c && !cg->coop_ws) {
     DeviceGuard g(cg->ctx->device);
     CGX_HIP(hipMalloc(&cg->coop_ws, sizeof(CoopWs)));
-    CGX_HIP(hipMalloc(&cg->coop_rg, (size_t)cg->n * 48));
     if (const char *e = std::getenv("CGX_COOP_TRACE"); e && std::atoi(e)) {
       CGX_HIP(hipMalloc(&cg->coop_trace, kCoopTraceWords * sizeof(unsigned long long)));
       CGX_HIP(hipMemset(cg->coop_trace, 0, kCoopTraceWords * sizeof(unsigned long long)));
@@ -2205,6 +2560,10 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     cg->coop_ticks = (long long)clk_khz * 1000 * 2;  // 2 s: a resident grid never waits so long
     if (const char *e = std::getenv("CGX_COOP_TIMEOUT_MS"))
       cg->coop_ticks = (long long)clk_khz * std::max(1, std::atoi(e));
+  }
+  if (c && cg->coop_tagr && !stream && !cg->coop_rg) {  // the tagged form's p / r granules
+    DeviceGuard g(cg->ctx->device);
+    CGX_HIP(hipMalloc(&cg->coop_rg, (size_t)cg->n * 48));
   }
   cg->coop = c;
   if (c) {

@@ -37,13 +37,17 @@
 // the flag); one wave per workgroup sweeps all granules until every tag is
 // this body's; every load of handed-off data is an agent-scope atomic load.
 // No workgroup index, dispatch order or XCD placement enters the protocol.
-// The grid is one workgroup per CU at most (kCoopMaxG <= CUs / 2, so every
-// workgroup is resident), every spin is bounded by the wall clock, and a
+// The grid is one workgroup per CU at most (G <= min(kCoopMaxG, CUs)), and
+// cg_coop refuses a launch the occupancy API does not place whole (every
+// workgroup must be resident at once); every spin is bounded by the wall
+// clock, and a
 // workgroup that gives up raises CoopWs::tmo so the others leave too
 // (CgScalars::stopped = 4).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "cgx_internal.h"
 
@@ -598,7 +602,9 @@ __global__ __launch_bounds__(1024, 1) void k_cg_coop_st(
       const int base = bn, E = en;
       double acc = 0.0;
       double pr[P];
-      if (E <= PW) {
+      // jj / vv hold this chunk only when load() ran for it (0 < E <= PW); an
+      // empty chunk (past n) must not gather through stale indices
+      if (E > 0 && E <= PW) {
 #pragma unroll
         for (int z = 0; z < P; ++z) pr[z] = vv[z] * pk(jj[z]);
       }
@@ -712,6 +718,26 @@ int coop_stream_rows(int64_t n, int want, int max_g) {
   return 0;
 }
 
+// every workgroup of a G-workgroup launch of fn resident at once: the
+// occupancy API's workgroups per CU x the device's CUs (cached per kernel)
+static bool coop_resident(const void *fn, int NT, int G) {
+  static std::mutex mu;
+  static std::map<std::pair<const void *, int>, int> cap;
+  std::lock_guard<std::mutex> lk(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const auto key = std::make_pair(fn, dev);
+  auto it = cap.find(key);
+  if (it == cap.end()) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+    it = cap.emplace(key, per_cu * cus).first;
+  }
+  return G <= it->second;
+}
+
 hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
                    unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
@@ -726,14 +752,19 @@ hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const 
   if (e == hipSuccess && tagged) e = hipMemsetAsync(g, 0, (size_t)n * 48, s);
   if (e != hipSuccess) return e;
   unsigned long long *pg = g, *rg = g ? g + 4 * n : nullptr;
+#define CGX_COOP_FIT(K, TT) \
+  if (!coop_resident((const void *)K, TT, G)) return hipErrorCooperativeLaunchTooLarge
 #define CGX_COOP_WT(RR, TT)                                                                 \
+  CGX_COOP_FIT((k_cg_coop_wt<RR, TT>), TT);                                                 \
   k_cg_coop_wt<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
                                         ticks, trace, nap, stall)
 #define CGX_COOP_TG(RR, TT)                                                                 \
+  CGX_COOP_FIT((k_cg_coop_tg<RR, TT>), TT);                                                 \
   k_cg_coop_tg<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, pg, rg, st, slot0, m, \
                                         cw, ticks, trace, nap, stall)
 #define CGX_COOP_ST(RR)                                                                     \
   case RR:                                                                                  \
+    CGX_COOP_FIT(k_cg_coop_st<RR>, 1024);                                                   \
     k_cg_coop_st<RR><<<G, 1024, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
                                         ticks, trace, nap, stall);                          \
     break;
@@ -763,6 +794,7 @@ hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const 
   }
 #undef CGX_COOP_WT
 #undef CGX_COOP_TG
+#undef CGX_COOP_FIT
   return hipGetLastError();
 }
 

@@ -111,6 +111,27 @@ constexpr int kYM = 16777216;
 constexpr int kC16 = 128;
 constexpr int kVtMax = 8;
 constexpr int kVtWidthMask = 0xffff;
+// Lean stencil walk (variant bit kVL; DESIGN.md §4 "lean stencil walk"): a
+// slice whose offset pattern is a subset of a stencil's {-D, -a, -1, 0, +1,
+// +a, +D} (a = 0: the 2-D {-D, -1, 0, +1, +D}) and whose template chunk gives
+// every row of a slot the same value (rows 0 and 1 of a lane alike) has no
+// per-row data at all: its class (template, pattern) holds the seven values
+// and which slots are present. The only entries a row of such a slice may
+// lack are the x-line ends' -1 (lane 0, row 0) and +1 (lane 63, row 1); the
+// kernel then multiplies v by z = -copysign(0, v), whose product -0.0 is the
+// identity of +, so the row's sum is the one that skips the entry, bit for
+// bit (v finite). Classes per slice: one byte, 0xff for the slices that run
+// the per-slice value-code form, laid out wave-major for the launch's grid
+// (row of wave w of XCD group g: (g step + w) * nst, step = grid / 2 waves).
+constexpr int kVL = 33554432;
+constexpr int kVlMaxCls = 32;
+struct VlClass {
+  double v[8];      // value of canonical slot j: -D, -a, -1, 0, +1, +a, +D
+  double zlo, zhi;  // -copysign(0, v[2]), -copysign(0, v[4])
+  int plo, phi;     // lane 0's row 0 has its -1 entry; lane 63's row 1 its +1
+  int pres;         // bit 0 -D, 1 -a, 2 +a, 3 +D present (-1, 0, +1 always are)
+  int pad;
+};
 
 struct SellSlice {
   int64_t voff;  // first value of the slice (entries)
@@ -171,6 +192,13 @@ struct CsrDev {
   // block b stores col[k] - rb[b] (every such delta fits int16; null when
   // one does not or the copy was not built)
   const short *col16 = nullptr;
+  // lean stencil walk (kVL, cgx_abi.cpp build_lean): the class bytes in the
+  // wave-major layout of a vl_grid-workgroup launch (vl_nst bytes per wave),
+  // the class table, the stencil's D and a; `lean`: the loop's SpMV runs it
+  const unsigned char *vl_cls = nullptr;
+  const VlClass *vl_tab = nullptr;
+  int vl_grid = 0, vl_nst = 0, vl_D = 0, vl_a = 0;
+  bool lean = false;
 };
 
 // The templates apply to the pipelined 4-bit value-code walks (bits 524288,
@@ -186,6 +214,11 @@ __host__ __device__ inline bool ym_active(const CsrDev &A) {
 __host__ __device__ inline bool vt_active(const CsrDev &A) {
   return (A.variant & kVT) && A.sl_t && A.vct && A.nvt > 0 && A.svc4 && A.svc && A.sl &&
          A.sell_kind && A.sell_maxw <= 8 && (A.variant & 524288) && (A.variant & 262144);
+}
+// the loop's k_spmv_dot is the lean walk (its generic slices run the
+// template value-code form, so vt_active holds too)
+__host__ __device__ inline bool vl_active(const CsrDev &A) {
+  return A.lean && A.vl_cls && A.vl_tab && A.vl_grid > 0 && vt_active(A);
 }
 
 template <typename T> struct Launch {
@@ -203,6 +236,8 @@ template <typename T> struct Launch {
                              int slot, RedWs<T> *ws, hipStream_t s, int rev = 0);
   static hipError_t spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                      CgScalars<T> *st, RedWs<T> *ws, hipStream_t s);
+  // the lean stencil walk's resident workgroups (its grid's upper bound)
+  static int lean_resident();
   // np_pap > 0: p.Ap from the spmv_dot partials; 0: from st->pAp[slot]
   static hipError_t update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s, bool fused = false, int np_pap = 0,

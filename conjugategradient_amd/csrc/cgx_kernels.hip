@@ -307,6 +307,11 @@ struct CsrArgs {
   const unsigned long long *vct;
   const short *__restrict__ col16;  // 16-bit column deltas (kC16)
   int nvt;
+  // lean stencil walk (kVL): wave-major class bytes, class table, bytes per
+  // wave row, the stencil's D and a
+  const unsigned char *__restrict__ vl_cls;
+  const VlClass *vl_tab;
+  int vl_nst, vl_D, vl_a;
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -1702,6 +1707,104 @@ __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, E
                                      slice_at(A, A.rev ? lo + end - 1 - s : s), vt);
 }
 
+
+// Lean stencil walk (kVL; cgx_internal.h, DESIGN.md §4 "lean stencil walk").
+// The launch's grid G (a multiple of 8) is the one the class bytes were laid
+// out for; the waves of XCD group g walk its eighth of the slices with
+// step G / 2, like sell_range, so with G / 2 equal to the slices of a plane
+// (D = 128 G / 2 rows) a wave's +-D gathers are the lines it loads as its
+// own centers one step before and after, still in its XCD's L2
+// (tools/probes/stencil_floor.hip: 42 us at 256^3 with G = 1024 against 61
+// with G = 2048). A lean slice (class byte c < 0xff) issues its center pair,
+// its present +-D / +-a pairs (an absent slot re-reads the center, an L1
+// hit, and is not added) and the scalar edges x[first - 1], x[first + 128]
+// at once, waits once, takes +-1 from the neighbour lanes (DPP) and sums
+// both rows in the canonical slot order, which is their CSR order: Ap is the
+// per-row loop's, bit for bit. Its values come from the class table (scalar
+// loads that hit the constant cache): no code word, no dictionary read, no
+// per-slot select. Other slices (boundary lines and planes of another
+// pattern, chunks no template matched) run sellpv_slice2 on the template
+// value codes. The class bytes of 256 steps come in one dword per lane and
+// are read with v_readlane: no scalar load per slice waits on the memory
+// behind the constant cache.
+template <typename T, class Epi, class Gather>
+__device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi &epi,
+                                          const T *__restrict__ vd,
+                                          const unsigned long long *vt) {
+  constexpr int VG = 8192 | 32768 | 262144 | 524288 | kVT | 2;  // the generic slices' form
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = (int)gridDim.x, b = (int)blockIdx.x, g = b & 7;
+  const int step = (G >> 3) * 4, w = (b >> 3) * 4 + wid;
+  const int nsl = (int)A.nsl;
+  const int lo = (int)(((int64_t)nsl * g) >> 3), end = (int)(((int64_t)nsl * (g + 1)) >> 3);
+  // rows of the reversed sweep (A.rev: slice lo + end - 1 - s at walk
+  // position s, as sell_range's walkers) follow the forward ones
+  const unsigned *__restrict__ row = reinterpret_cast<const unsigned *>(
+      A.vl_cls + (int64_t)((A.rev ? 8 * step : 0) + g * step + w) * A.vl_nst);
+  const int nw = A.vl_nst >> 2;  // class words of this wave's row
+  const auto *tab = (const __attribute__((address_space(4))) VlClass *)A.vl_tab;
+  const int nxm1 = (int)A.nx - 1;
+  const unsigned oD = (unsigned)A.vl_D * (unsigned)sizeof(T);
+  const unsigned oa = (unsigned)A.vl_a * (unsigned)sizeof(T);
+  unsigned cw = 0;
+  for (int s = lo + w, j = 0; s < end; s += step, ++j) {
+    if ((j & 255) == 0) {  // the classes of the next 256 steps, lane l: steps 4l .. 4l + 3
+      const int k = (j >> 2) + lane;
+      cw = k < nw ? row[k] : ~0u;
+    }
+    const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, (j & 255) >> 2);
+    const int c = (int)((word >> (8 * (j & 3))) & 0xffu);
+    const int si = A.rev ? lo + end - 1 - s : s;
+    if (c == 0xff) {
+      sellpv_slice2<T, VG, Epi, Gather>(A, x, epi, vd, si, vt);
+      continue;
+    }
+    const int pres = tab[c].pres;
+    const int r0 = si * (2 * kSellRows) + 2 * lane;
+    const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
+    const auto ct = x.pair_b(rb);
+    const auto gmD = x.pair_b(rb - ((pres & 1) ? oD : 0u));
+    const auto gma = x.pair_b(rb - ((pres & 2) ? oa : 0u));
+    const auto gpa = x.pair_b(rb + ((pres & 4) ? oa : 0u));
+    const auto gpD = x.pair_b(rb + ((pres & 8) ? oD : 0u));
+    const int fr = si * (2 * kSellRows);
+    const T elo = x.at_s(fr > 0 ? fr - 1 : 0);
+    const T ehi = x.at_s(fr + 2 * kSellRows <= nxm1 ? fr + 2 * kSellRows : nxm1);
+    T v[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) v[q] = T(tab[c].v[q]);
+    const T lo_e = tab[c].plo ? elo : T(tab[c].zlo);
+    const T hi_e = tab[c].phi ? ehi : T(tab[c].zhi);
+    const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
+    epi.pre2c(r0, r0 + 1, ct.x, ct.y);
+    T a0 = T(0), a1 = T(0);
+    if (pres & 1) {
+      a0 = a0 + v[0] * gmD.x;
+      a1 = a1 + v[0] * gmD.y;
+    }
+    if (pres & 2) {
+      a0 = a0 + v[1] * gma.x;
+      a1 = a1 + v[1] * gma.y;
+    }
+    a0 = a0 + v[2] * left;
+    a1 = a1 + v[2] * ct.x;
+    a0 = a0 + v[3] * ct.x;
+    a1 = a1 + v[3] * ct.y;
+    a0 = a0 + v[4] * ct.y;
+    a1 = a1 + v[4] * right;
+    if (pres & 4) {
+      a0 = a0 + v[5] * gpa.x;
+      a1 = a1 + v[5] * gpa.y;
+    }
+    if (pres & 8) {
+      a0 = a0 + v[6] * gpD.x;
+      a1 = a1 + v[6] * gpD.y;
+    }
+    epi.row2(r0, a0, a1, true, true);
+  }
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
@@ -1981,6 +2084,24 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
   // this workgroup's share of p.Ap; k_update_r sums the partials
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
+// k_spmv_dot in the lean stencil walk (kVL): the same epilogue and partials
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_lean(CsrArgs A, const T *__restrict__ p,
+                                                      T *__restrict__ Ap, CgScalars<T> *st,
+                                                      int slot, RedWs<T> *ws) {
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T *__restrict__ src = static_cast<const T *>(A.svdict);
+  for (int i = threadIdx.x; i < kVcDict; i += kBlock) sm.vdict[i] = src[i];
+  for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) sm.vt[i] = A.vct[i];
+  __syncthreads();
+  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
+  spmv_lean<T>(A, GatherX<T>{p}, e, sm.vdict, sm.vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
@@ -2764,6 +2885,13 @@ inline CsrArgs args(const CsrDev &A) {
     a.nvt = A.nvt;
   }
   a.col16 = A.col16;
+  if (vl_active(A)) {
+    a.vl_cls = A.vl_cls;
+    a.vl_tab = A.vl_tab;
+    a.vl_nst = A.vl_nst;
+    a.vl_D = A.vl_D;
+    a.vl_a = A.vl_a;
+  }
   return a;
 }
 
@@ -3302,11 +3430,32 @@ hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *
                               hipStream_t s) {
   CGX_CSR_ONEOFF(k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws, tol, cap);
 }
+template <typename T> int Launch<T>::lean_resident() {
+  static std::mutex mu;
+  static std::map<int, int> cache;  // device -> workgroups
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int nb = 0, cus = 0, res = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)&k_spmv_lean<T>, kBlock,
+                                                   0) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+    res = nb * cus;
+  cache[dev] = res;
+  return res;
+}
 template <typename T>
 hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
                                int slot, RedWs<T> *ws, hipStream_t s, int rev) {
   CsrArgs a = args(A);
   a.rev = rev;
+  if (vl_active(A)) {  // the lean stencil walk: its own grid (the class layout's)
+    hipLaunchKernelGGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
+                       ws);
+    return hipGetLastError();
+  }
   const int v = spmv_variant<T>(A);
   const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), v);
   CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
@@ -3335,6 +3484,13 @@ template <typename T> int Launch<T>::slice_grid(const CsrDev &A, int count) {
 template <typename T>
 hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap,
                                        CgScalars<T> *st, RedWs<T> *ws, hipStream_t s) {
+  if (v & kVL) {  // the lean walk (A's class layout)
+    CsrDev d = A;
+    d.variant = v & ~kVL;
+    d.lean = true;
+    if (!vl_active(d)) return hipErrorInvalidValue;
+    return spmv_dot(d, p, Ap, st, 0, ws, s, 0);
+  }
   const int vv = spmv_variant<T>(A, v);
   const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), vv);
   switch (vv) {  // timing ablations (bits 16/32) exist for this kernel only
@@ -3551,6 +3707,7 @@ hipError_t Launch<T>::rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipSt
   CGX_LAUNCH(k_rr_settle<T>, 1, st, ws, np_rr);
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
+  if (vl_active(A)) return A.vl_grid;
   return cap_resident<T>(grid_rows(A.nrb), spmv_variant<T>(A));  // = spmv_dot's grid
 }
 template <typename T> int Launch<T>::update_parts(int64_t n) {
@@ -3674,8 +3831,10 @@ hipError_t Launch<T>::sell_pack(const CsrDev &A, const T *val, T *sval, hipStrea
              A.rowptr, val, A.sl, sval);
 }
 
+// (kVL added when the loop's SpMV is the lean walk)
 int launch_variant(const CsrDev &A, int dtype) {
-  return dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A);
+  return (dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A)) |
+         (vl_active(A) ? kVL : 0);
 }
 
 bool launch_variant_ok(const CsrDev &A, int dtype) {

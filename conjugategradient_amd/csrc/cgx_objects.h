@@ -161,6 +161,12 @@ struct cgx_csr {
   void *d_sell_sl_t = nullptr, *d_vct = nullptr;       // value-code templates (kVT)
   int64_t vt_slices = 0;                               // slices that read a template
   void *d_col16 = nullptr;  // CSR-stream 16-bit column deltas (cgx::CsrDev::col16)
+  // lean stencil walk (kVL, cgx_abi.cpp build_lean): per-slice classes in
+  // slice order (host), their device layout for grid dev.vl_grid, the table
+  std::vector<int> sell_pool;               // the SELL-P pattern pool (host copy)
+  std::vector<unsigned char> vl_slice_cls;  // class per slice (0xff: per-slice form)
+  int vl_ncls = 0;
+  void *d_vl_cls = nullptr, *d_vl_tab = nullptr;
   // partitioned SELL matrix: slices without ghost columns, then those with
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;

@@ -111,6 +111,15 @@ int cgx_csr_value_codes(cgx_csr *csr, int *n_values);
  * code chunks stored once and read from LDS, and the slices that use one
  * (0 / 0: none). */
 int cgx_csr_templates(cgx_csr *csr, int *n_templates, int64_t *slices);
+/* The lean stencil walk (variant bit 33554432, kept by the autotune where it
+ * wins or requested with cgx_csr_set_variant): slices whose pattern is a
+ * subset of one stencil's {-D, -a, -1, 0, +1, +a, +D} and whose template
+ * chunk holds one value per slot, summed from per-class values with no
+ * per-row stream. *classes: distinct (template, pattern) classes, *slices:
+ * slices that run it, *grid: its launch's workgroups, *D / *a: the stencil's
+ * offsets (all 0 when the matrix has none built). Replaces nothing in the
+ * reference: a format of VectorOperations.hpp:438-466's SpMV. */
+int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, int *D, int *a);
 /* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
  * *stride = slices (of 128 rows) between a slice and its +-D neighbour
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D

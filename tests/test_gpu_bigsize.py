@@ -1,11 +1,11 @@
 """The two BASELINE configs beyond 16.8 M rows or without a stencil:
 
 * 512^3 on one GPU (134 M rows, the 8-GPU config's whole problem): the
-  production SpMV format (value-code stencil SELL-P) equals the general
-  CSR-stream kernel bit for bit on the device (both sum each row in CSR
-  order), and the deferred-x iteration (mode 3) equals the three-kernel one
-  (mode 1) bit for bit over 12 bodies — size-independent properties, since
-  the CPU oracle would take minutes per body here.
+  production SpMV format (value-code stencil SELL-P) equals the oracle's
+  per-row loop and the general CSR-stream kernel bit for bit, five CG bodies
+  match the oracle's (OpenMP, 16 threads) at rel <= 1e-10, and the
+  deferred-x iteration (mode 3) equals the three-kernel one (mode 1) bit for
+  bit over 12 bodies.
 * the G3_circuit stand-in at its real size (1,585,478 rows, irregular rows,
   thousands of distinct values -> CSR-stream): SpMV bit-exact against the
   oracle, and a solve to a tight relative tolerance held to the bars of
@@ -60,6 +60,35 @@ def test_512cubed_formats_and_modes_agree(queue):
         del cg
     assert np.isfinite(xs[0]).all()
     np.testing.assert_array_equal(xs[0], xs[1])
+
+
+def test_512cubed_matches_oracle(queue, oracle):
+    # config 4's whole problem against the oracle itself (one CPU pass over
+    # 134 M rows for the SpMV; five bodies of the OpenMP restatement of
+    # CG.hpp:359-436): the production SpMV bit for bit, CG at rel <= 1e-10
+    # (the dots' summation order differs; every other value is rounded alike)
+    rp, cl, vl = oracle.poisson(3, 512, 512, 512)
+    n = len(rp) - 1
+    m = cga.Matrix.poisson(queue, 3, 512, 512, 512)
+    assert m.N() == n and m.NNZ() == len(vl)
+    prod = _variant(m)
+    x = np.random.default_rng(5120).standard_normal(n)
+    y = cga.Vector(queue, n)
+    cga.VectorOperations(queue).spmv(m, cga.Vector(queue, x), y, m.NNZ(), count=n)
+    np.testing.assert_array_equal(y.to_numpy(), oracle.spmv(rp, cl, vl, x),
+                                  err_msg=f"variant {prod}")
+    del y, x
+    b = np.arange(1, n + 1, dtype=np.float64)
+    cg = cga.CG(queue)
+    cg.setMatrix(m)
+    cg.setTarget(b)
+    cg.solve(0.0, max_iter=5)
+    assert cg.iterations == 5
+    xg = cg.extract()
+    del cg
+    xr, res = oracle.cg_solve_omp(rp, cl, vl, b, 0.0, 16, max_iter=5)
+    assert res.iterations == 5
+    assert rel(xg, xr) <= 1e-10, rel(xg, xr)
 
 
 G3_N = 1_585_478
