@@ -360,7 +360,7 @@ def run(args) -> None:
     check(L.cgx_csr_stream_bytes(A, C.byref(sbytes)))
     ntpl, tpl_slices = C.c_int(0), C.c_int64(0)
     check(L.cgx_csr_templates(A, C.byref(ntpl), C.byref(tpl_slices)))
-    lean = [C.c_int(0), C.c_int64(0), C.c_int(0), C.c_int(0), C.c_int(0)]
+    lean = [C.c_int(0), C.c_int64(0), C.c_int(0), C.c_int(0), C.c_int(0), C.c_int(0)]
     check(L.cgx_csr_lean_info(A, *[C.byref(v) for v in lean]))
     lean_on = bool(variant.value & KVL)
     cg = C.c_void_p()
@@ -531,7 +531,8 @@ def run(args) -> None:
                        "lean_walk": (
                            {"classes": lean[0].value, "slices": lean[1].value,
                             "slices_total": (n_local + 127) // 128, "grid": lean[2].value,
-                            "D": lean[3].value, "a": lean[4].value, "in_use": lean_on}
+                            "D": lean[3].value, "a": lean[4].value,
+                            "chunked_walk": bool(lean[5].value), "in_use": lean_on}
                            if lean[0].value else None)},
             "roofline": roof,
             "csr_general": general,

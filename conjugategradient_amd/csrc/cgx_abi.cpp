@@ -978,6 +978,7 @@ void free_lean(cgx_csr *A) {
   A->dev.vl_cls = nullptr;
   A->dev.vl_tab = nullptr;
   A->dev.vl_grid = A->dev.vl_nst = A->dev.vl_D = A->dev.vl_a = 0;
+  A->dev.vl_P = A->dev.vl_K = 0;
   A->dev.lean = false;
   A->vl_slice_cls.clear();
   A->vl_ncls = 0;
@@ -1631,6 +1632,12 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
   if (A->vl_slice_cls.empty() || tab.empty() || G < 8 || G % 8) return CGX_EINVAL;
   const int64_t nsl = A->dev.nsl;
   const int step = G / 2;
+  // the chunked walk (spmv_lean) where a plane holds several chunks of step
+  // slices and every XCD group's eighth is whole planes
+  const int D = A->dev.vl_D;
+  const int64_t K = D % (2 * kSellRows) == 0 ? D / (2 * kSellRows) : 0;
+  const bool chunked = K > step && K % step == 0 && nsl % (8 * K) == 0;
+  const int64_t P = chunked ? nsl / 8 / K : 0;
   int64_t nst = 0;
   for (int g = 0; g < 8; ++g) {
     const int64_t lo = (nsl * g) >> 3, end = (nsl * (g + 1)) >> 3;
@@ -1645,8 +1652,18 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
       for (int w = 0; w < step; ++w) {
         unsigned char *row = h.data() + (size_t)((int64_t)(rev * 8 * step + g * step + w) * nst);
         int64_t j = 0;
-        for (int64_t q = lo + w; q < end; q += step)
-          row[j++] = A->vl_slice_cls[(size_t)(rev ? lo + end - 1 - q : q)];
+        for (int64_t q = lo + w, zp = 0, cb = 0; q < end; ++j) {
+          row[j] = A->vl_slice_cls[(size_t)(rev ? lo + end - 1 - q : q)];
+          if (!chunked) {
+            q += step;
+            continue;
+          }
+          if (++zp == P) {
+            zp = 0;
+            cb += step;
+          }
+          q = cb >= K ? end : lo + zp * K + cb + w;
+        }
       }
     }
   void *dc = nullptr, *dt = nullptr;
@@ -1670,6 +1687,8 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
   A->dev.vl_tab = (const VlClass *)dt;
   A->dev.vl_grid = G;
   A->dev.vl_nst = (int)nst;
+  A->dev.vl_P = (int)P;
+  A->dev.vl_K = chunked ? (int)K : 0;
   A->vl_ncls = (int)tab.size();
   return CGX_OK;
 }
@@ -1912,8 +1931,10 @@ extern "C" int cgx_csr_templates(cgx_csr *A, int *n_templates, int64_t *slices) 
 }
 
 extern "C" int cgx_csr_lean_info(cgx_csr *A, int *classes, int64_t *slices, int *grid, int *D,
-                                 int *a) {
-  CGX_REQUIRE(A && classes && slices && grid && D && a, CGX_EINVAL, "NULL argument");
+                                 int *a, int *chunked) {
+  CGX_REQUIRE(A && classes && slices && grid && D && a && chunked, CGX_EINVAL,
+              "NULL argument");
+  *chunked = A->dev.vl_cls && A->dev.vl_P > 0 ? 1 : 0;
   const bool on = A->dev.vl_cls != nullptr;
   int64_t cnt = 0;
   if (on)
@@ -2032,15 +2053,15 @@ int autotune_spmv(cgx_csr *A) {
       set_error("$CGX_SPMV_VARIANT=%s: %s", env, why.c_str());
       return CGX_EINVAL;
     }
-    if ((v & kVL) && G > 0) {
+    if ((v & kVL) && colon) {  // "V:G" (G 0: the first grid candidate)
       std::vector<VlClass> tab;
       if (build_lean_classes(A, tab) != CGX_OK || tab.empty() ||
-          build_lean_layout(A, tab, G) != CGX_OK) {
+          build_lean_layout(A, tab, G > 0 ? G : lean_grids(A).front()) != CGX_OK) {
         set_error("$CGX_SPMV_VARIANT=%s: no lean walk at grid %d", env, G);
         return CGX_EINVAL;
       }
     }
-    if (!(v & (2048 | 8192))) free_sell(A);
+    if (!(v & (2048 | 8192 | kVL))) free_sell(A);
     return CGX_OK;
   }
   const int64_t bytes = A->dev.nnz * (int64_t)(dtype_size(A->dtype) + sizeof(int));
@@ -2186,6 +2207,9 @@ int autotune_spmv(cgx_csr *A) {
   std::vector<VlClass> vtab;
   int lean_G = 0;
   if (e == hipSuccess && A->dev.sl_t && build_lean_classes(A, vtab) == CGX_OK && !vtab.empty()) {
+    // candidates: the grids (a software-pipelined form, two slices' gathers in
+    // flight per wave, measured slower at 256^3 and 512^3 in the loop:
+    // 747 against 631 us at 512^3, profiles/r04_lean_pipe512.log; not built)
     const std::vector<int> gs = lean_grids(A);
     std::vector<float> tl(gs.size() + 1, 1e30f);  // [0]: the incumbent
     for (int round = 0; round < 3 && e == hipSuccess; ++round)
@@ -2224,10 +2248,14 @@ int autotune_spmv(cgx_csr *A) {
         if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
         if (e == hipSuccess) tl[k] = std::min(tl[k], tot);
       }
+    // the plane-matched grid (first candidate when there is one) unless
+    // another is faster by more than 3%: isolated timings tie it with the
+    // resident grid at 256^3, and in the loop it wins at 512^3 (631 against
+    // 665 us, profiles/r04_lean_pipe512.log)
+    size_t kb = 0;
     for (size_t k = 1; k <= gs.size() && e == hipSuccess; ++k)
-      if (tl[k] < tl[0] && (lean_G == 0 || tl[k] < tl[(size_t)(std::find(gs.begin(), gs.end(),
-                                                                          lean_G) - gs.begin()) + 1]))
-        lean_G = gs[k - 1];
+      if (tl[k] < (k > 1 && kb == 1 ? tl[kb] * 0.97f : tl[kb])) kb = k;
+    if (kb > 0) lean_G = gs[kb - 1];
   }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);

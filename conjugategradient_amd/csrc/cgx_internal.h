@@ -198,6 +198,7 @@ struct CsrDev {
   const unsigned char *vl_cls = nullptr;
   const VlClass *vl_tab = nullptr;
   int vl_grid = 0, vl_nst = 0, vl_D = 0, vl_a = 0;
+  int vl_P = 0, vl_K = 0;  // the chunked walk's planes per XCD group, slices per plane
   bool lean = false;
 };
 

@@ -312,6 +312,7 @@ struct CsrArgs {
   const unsigned char *__restrict__ vl_cls;
   const VlClass *vl_tab;
   int vl_nst, vl_D, vl_a;
+  int vl_P, vl_K;  // the chunked walk: planes per XCD group, slices per plane (0: natural)
 };
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
@@ -1748,7 +1749,22 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
   const unsigned oD = (unsigned)A.vl_D * (unsigned)sizeof(T);
   const unsigned oa = (unsigned)A.vl_a * (unsigned)sizeof(T);
   unsigned cw = 0;
-  for (int s = lo + w, j = 0; s < end; s += step, ++j) {
+  // the chunked walk (A.vl_P > 0; cgx_abi.cpp build_lean_layout): the
+  // group's eighth is P whole planes of K slices and step divides K; wave w
+  // walks chunk position w of chunk c through the P planes, chunk after
+  // chunk, so its +-D neighbours are its own centers one step away also
+  // when a plane is wider than the group's waves (512^3)
+  const int P = A.vl_P, K = A.vl_K;
+  int zp = 0, cb = 0;  // plane and chunk base of the chunked walk's step
+  auto next = [&](int s) {
+    if (P == 0) return s + step;
+    if (++zp == P) {
+      zp = 0;
+      cb += step;
+    }
+    return cb >= K ? end : lo + zp * K + cb + w;
+  };
+  for (int s = lo + w, j = 0; s < end; s = next(s), ++j) {
     if ((j & 255) == 0) {  // the classes of the next 256 steps, lane l: steps 4l .. 4l + 3
       const int k = (j >> 2) + lane;
       cw = k < nw ? row[k] : ~0u;
@@ -2214,6 +2230,51 @@ __global__ __launch_bounds__(kBlock, FdWaves<V>::w) void k_spmv_fd(
   const GatherP<T, NTP> g{r, pold, beta};
   EpiFD<T, NTP> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, g, e, sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
+// k_spmv_fd in the lean stencil walk (kVL): the gathers form p_k = r +
+// beta p_{k-1} from both vectors (GatherP), the epilogue stores p_k and Ap
+// (EpiFD); the same preamble (beta from the r.r partials, the record of the
+// previous body's r.r)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
+    CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
+    T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr) {
+  __shared__ SellLds<T> sm;
+  const int prev = (slot + 3) & 3;
+  const long long bodies = st->bodies;
+  const bool act = st->active[slot] != 0;
+  if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+  if (!act) {
+    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot) {
+      const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+      if (threadIdx.x == 0) {
+        st->rr[prev] = rr;
+        st->rxr[slot] = rr;
+      }
+    }
+    return;
+  }
+  T beta = T(0);
+  if (bodies > 0) {
+    const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+    beta = rr / st->rxr[prev];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->rr[prev] = rr;  // the record
+      st->rxr[slot] = rr;
+    }
+  }
+  const T *__restrict__ src = static_cast<const T *>(A.svdict);
+  for (int i = threadIdx.x; i < kVcDict; i += kBlock) sm.vdict[i] = src[i];
+  for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) sm.vt[i] = A.vct[i];
+  __syncthreads();
+  const GatherP<T> g{r, pold, beta};
+  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_lean<T>(A, g, e, sm.vdict, sm.vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
@@ -2891,6 +2952,8 @@ inline CsrArgs args(const CsrDev &A) {
     a.vl_nst = A.vl_nst;
     a.vl_D = A.vl_D;
     a.vl_a = A.vl_a;
+    a.vl_P = A.vl_P;
+    a.vl_K = A.vl_K;
   }
   return a;
 }
@@ -3597,6 +3660,7 @@ template <typename T> bool Launch<T>::fd_supported(const CsrDev &A) {
 // to rounding (the sum order of one dot), not bit for bit. Holding k_spmv_fd
 // to k_spmv_dot's waves per SIMD instead spilled 20-56 VGPRs to scratch.
 template <typename T> int Launch<T>::fd_parts(const CsrDev &A) {
+  if (vl_active(A)) return A.vl_grid;
   const int grid = grid_rows(A.nrb);
   const int r = spmv_fd_resident<T>(spmv_variant<T>(A));
   return (r > 0 && r < grid) ? r : grid;
@@ -3609,6 +3673,13 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   if (!k) return hipErrorInvalidValue;
   CsrArgs a = args(A);
   a.rev = rev;
+  if constexpr (std::is_same<T, double>::value) {
+    if (vl_active(A)) {  // the lean walk at its class layout's grid
+      hipLaunchKernelGGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
+                         Ap, st, slot, ws, np_rr);
+      return hipGetLastError();
+    }
+  }
   const T *val = (const T *)A.val;
   void *kargs[] = {&a, (void *)&val, (void *)&r, (void *)&pold, (void *)&pc, (void *)&Ap,
                    (void *)&st, (void *)&slot, (void *)&ws, (void *)&np_rr};

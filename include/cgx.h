@@ -117,9 +117,12 @@ int cgx_csr_templates(cgx_csr *csr, int *n_templates, int64_t *slices);
  * chunk holds one value per slot, summed from per-class values with no
  * per-row stream. *classes: distinct (template, pattern) classes, *slices:
  * slices that run it, *grid: its launch's workgroups, *D / *a: the stencil's
- * offsets (all 0 when the matrix has none built). Replaces nothing in the
- * reference: a format of VectorOperations.hpp:438-466's SpMV. */
-int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, int *D, int *a);
+ * offsets, *chunked: 1 when its waves walk chunks of a plane through the
+ * planes (planes wider than a grid step; all 0 when the matrix has none
+ * built). Replaces nothing in the reference: a format of
+ * VectorOperations.hpp:438-466's SpMV. */
+int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, int *D, int *a,
+                      int *chunked);
 /* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
  * *stride = slices (of 128 rows) between a slice and its +-D neighbour
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D

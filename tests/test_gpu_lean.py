@@ -22,10 +22,10 @@ KVL = 33554432
 
 
 def lean_info(m):
-    c, s, g, d, a = C.c_int(), C.c_int64(), C.c_int(), C.c_int(), C.c_int()
+    c, s, g, d, a, pp = C.c_int(), C.c_int64(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
     check(lib().cgx_csr_lean_info(m.schedule(), C.byref(c), C.byref(s), C.byref(g),
-                                  C.byref(d), C.byref(a)))
-    return c.value, s.value, g.value, d.value, a.value
+                                  C.byref(d), C.byref(a), C.byref(pp)))
+    return c.value, s.value, g.value, d.value, a.value, pp.value
 
 
 def variant(m):
@@ -49,20 +49,22 @@ CASES = {
     "p3d_128x96x40": ((3, 128, 96, 40), (12288, 128)),  # a slice is a whole x-line
     "p3d_256x32x24": ((3, 256, 32, 24), (8192, 256)),
     "p2d_1024x640": ((2, 1024, 640, 1), (1024, 0)),
+    # planes of 1,024 slices: the chunked walk where the grid's step is half a plane
+    "p3d_512x256x16": ((3, 512, 256, 16), (131072, 512)),
 }
 
 
 @pytest.mark.parametrize("case", list(CASES))
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_lean_spmv_bitexact(queue, oracle, case, dtype):
+def test_lean_spmv_bitexact(queue, oracle, monkeypatch, case, dtype):
     dims, (D, a) = CASES[case]
     rp, cl, vl = oracle.poisson(*dims)
     n = len(rp) - 1
+    # the walk forced at creation (its first grid candidate)
+    monkeypatch.setenv("CGX_SPMV_VARIANT", f"{KVL}:0")
     m = Matrix(queue, vl.astype(dtype), cl, rp, dtype=dtype)
-    check(lib().cgx_csr_set_sell(m.schedule(), 3))
-    check(lib().cgx_csr_set_variant(m.schedule(), KVL))
     assert variant(m) & KVL
-    ncls, nlean, grid, d, aa = lean_info(m)
+    ncls, nlean, grid, d, aa, chunked = lean_info(m)
     nsl = n // 128
     assert (d, aa) == (D, a)
     assert 1 <= ncls <= 32 and grid % 8 == 0 and grid > 0
@@ -100,7 +102,7 @@ def test_lean_mixed_with_the_per_slice_form(queue, oracle):
     m = Matrix(queue, vl, cl, rp)
     check(lib().cgx_csr_set_sell(m.schedule(), 3))
     check(lib().cgx_csr_set_variant(m.schedule(), KVL))
-    _, nlean, _, _, _ = lean_info(m)
+    _, nlean, _, _, _, _ = lean_info(m)
     assert nlean <= n // 128 - len(odd)
     x = np.random.default_rng(3).standard_normal(n)
     np.testing.assert_array_equal(spmv(queue, m, x, np.float64), oracle.spmv(rp, cl, vl, x))
