@@ -1693,24 +1693,25 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
   return CGX_OK;
 }
 
-// The lean walk's grid candidates: G / 2 waves per XCD step; with the step
-// a plane's slices K = D / 128 (or K / 2, K / 4 ...) the +-D gathers are the
-// wave's own centers one (two, four) steps away. Capped by the resident
-// workgroups; the largest resident grid is always a candidate.
-static std::vector<int> lean_grids(const cgx_csr *A) {
+// The lean walk's grid: G / 2 waves per XCD step; with the step a plane's
+// slices K = D / 128 (or K / 2, K / 4 ...) the +-D gathers are the wave's
+// own centers one (two, four) steps away, hits in its XCD's L2. That grid
+// when it keeps at least half the resident workgroups, else the resident
+// cap (a 2-D stencil's +-D, a few slices away, sit inside any step).
+// Measured in the loop (profiles/r04_lean_pipe512.log): 512^3 631 us at the
+// plane-matched 1,024 against 665 at 1,280; at 256^3 the two tie (55.8 /
+// 56.4 us).
+static int lean_grid(const cgx_csr *A) {
   const int res = A->dtype == CGX_F32 ? Launch<float>::lean_resident()
                                       : Launch<double>::lean_resident();
   const int cap = std::max(8, std::min(res, kMaxGrid) / 8 * 8);
-  std::vector<int> gs{cap};
   const int D = A->dev.vl_D;
   if (D > 0 && D % (2 * kSellRows) == 0) {
     int G = 2 * (D / (2 * kSellRows));
     while (G > cap && G % 16 == 0) G /= 2;
-    // first (the default of a request) when it keeps at least half the chip
-    if (G <= cap && G >= 64 && G % 8 == 0 && G != cap)
-      gs.insert(2 * G >= cap ? gs.begin() : gs.end(), G);
+    if (G <= cap && 2 * G >= cap && G % 8 == 0) return G;
   }
-  return gs;
+  return cap;
 }
 
 // build the lean walk's classes and, at grid G (0: the first candidate), its
@@ -1718,7 +1719,7 @@ static std::vector<int> lean_grids(const cgx_csr *A) {
 static bool build_lean(cgx_csr *A, int G = 0) {
   std::vector<VlClass> tab;
   if (build_lean_classes(A, tab) != CGX_OK || tab.empty()) return false;
-  if (G == 0) G = lean_grids(A).front();
+  if (G == 0) G = lean_grid(A);
   return build_lean_layout(A, tab, G) == CGX_OK;
 }
 // the variant under the lean walk: its generic slices' form (4-bit value
@@ -2056,7 +2057,7 @@ int autotune_spmv(cgx_csr *A) {
     if ((v & kVL) && colon) {  // "V:G" (G 0: the first grid candidate)
       std::vector<VlClass> tab;
       if (build_lean_classes(A, tab) != CGX_OK || tab.empty() ||
-          build_lean_layout(A, tab, G > 0 ? G : lean_grids(A).front()) != CGX_OK) {
+          build_lean_layout(A, tab, G > 0 ? G : lean_grid(A)) != CGX_OK) {
         set_error("$CGX_SPMV_VARIANT=%s: no lean walk at grid %d", env, G);
         return CGX_EINVAL;
       }
@@ -2201,30 +2202,28 @@ int autotune_spmv(cgx_csr *A) {
     if (ap) (void)hipFree(ap);
     if (e == hipSuccess && tf[1] < tf[0]) best_v = pair[1];
   }
-  // The lean stencil walk (kVL) at each of its grid candidates against the
-  // winner so far, interleaved rounds as above (its generic slices run the
-  // template value-code form, its base variant)
+  // The lean stencil walk (kVL) at its grid against the winner so far,
+  // interleaved rounds as above (its generic slices run the template
+  // value-code form, its base variant). (A software-pipelined form, two
+  // slices' gathers in flight per wave, measured slower in the loop: 747
+  // against 631 us at 512^3, profiles/r04_lean_pipe512.log; not built.)
   std::vector<VlClass> vtab;
   int lean_G = 0;
-  if (e == hipSuccess && A->dev.sl_t && build_lean_classes(A, vtab) == CGX_OK && !vtab.empty()) {
-    // candidates: the grids (a software-pipelined form, two slices' gathers in
-    // flight per wave, measured slower at 256^3 and 512^3 in the loop:
-    // 747 against 631 us at 512^3, profiles/r04_lean_pipe512.log; not built)
-    const std::vector<int> gs = lean_grids(A);
-    std::vector<float> tl(gs.size() + 1, 1e30f);  // [0]: the incumbent
+  // A 2-D plane-march winner runs the loop in mode 4 (fd_auto: two kernels
+  // per body, the p update inside the march's SpMV), which the lean walk's
+  // mode 3 does not beat (4096^2: 4,983 against 5,187-5,372 it/s,
+  // profiles/r04a_configs.log against r03p): it is not offered there.
+  const bool march2d = (best_v & 2097152) && A->dev.march_k > 0 && A->dev.march_a == 0;
+  if (e == hipSuccess && A->dev.sl_t && !march2d && build_lean_classes(A, vtab) == CGX_OK &&
+      !vtab.empty()) {
+    const int G = lean_grid(A);
+    if (build_lean_layout(A, vtab, G) != CGX_OK) e = hipErrorOutOfMemory;
+    float tl[2] = {1e30f, 1e30f};  // the incumbent, the lean walk
     for (int round = 0; round < 3 && e == hipSuccess; ++round)
-      for (size_t k = 0; k <= gs.size() && e == hipSuccess; ++k) {
+      for (int k = 0; k < 2 && e == hipSuccess; ++k) {
         CsrDev dv = A->dev;
-        dv.variant = best_v;
-        if (k > 0) {
-          if (build_lean_layout(A, vtab, gs[k - 1]) != CGX_OK) {
-            e = hipErrorOutOfMemory;
-            break;
-          }
-          dv = A->dev;
-          dv.variant = kVlBase;
-          dv.lean = true;
-        }
+        dv.variant = k ? kVlBase : best_v;
+        dv.lean = k == 1;
         float tot = 0;
         for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
           if (rep == 1) e = hipEventRecord(e0, s);
@@ -2248,14 +2247,7 @@ int autotune_spmv(cgx_csr *A) {
         if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
         if (e == hipSuccess) tl[k] = std::min(tl[k], tot);
       }
-    // the plane-matched grid (first candidate when there is one) unless
-    // another is faster by more than 3%: isolated timings tie it with the
-    // resident grid at 256^3, and in the loop it wins at 512^3 (631 against
-    // 665 us, profiles/r04_lean_pipe512.log)
-    size_t kb = 0;
-    for (size_t k = 1; k <= gs.size() && e == hipSuccess; ++k)
-      if (tl[k] < (k > 1 && kb == 1 ? tl[kb] * 0.97f : tl[kb])) kb = k;
-    if (kb > 0) lean_G = gs[kb - 1];
+    if (e == hipSuccess && tl[1] < tl[0]) lean_G = G;
   }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);

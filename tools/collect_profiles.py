@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy a tools/gpu_r3.sh run's summaries from gpurun_out/<tag>/ into
+"""Copy a tools/gpu_record.sh run's summaries from gpurun_out/<tag>/ into
 profiles/<prefix>_* (tracked): the GPU test log, smoke, the driver-command
 bench line, the rocprofv3 --kernel-trace --stats summary of that command,
 per-kernel HBM bytes from its FETCH_SIZE / WRITE_SIZE PMC passes, and the
@@ -35,7 +35,7 @@ for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
 if sums:
     out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs of "
                      "'python3 bench.py --no-cpu --no-general --steps 10 --warmup 2 "
-                     "--profile-steps 0' (tools/gpu_r3.sh); per dispatch (2 x FETCH_SIZE + "
+                     "--profile-steps 0' (tools/gpu_record.sh); per dispatch (2 x FETCH_SIZE + "
                      "WRITE_SIZE) x 1024 B (gfx950 FETCH correction, MI355X_MICROARCH.md)",
            "run": tag,
            "dispatches": {k: {c: v[1] for c, v in d.items()} for k, d in sums.items()},

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 GPU record: the gpu test suite (as the driver runs it), smoke, the
+# The round's GPU record: the gpu test suite (as the driver runs it), smoke, the
 # driver's bench command, rocprofv3 --kernel-trace --stats of that same
 # command, FETCH_SIZE / WRITE_SIZE PMC passes (separate runs), the per-config
 # lines. Stops at the first failing GPU step. Outputs in gpurun_out/$TAG.
-#   tools/gpu_r3.sh TAG [quick]     (quick: skip pytest)
+#   tools/gpu_record.sh TAG [quick]     (quick: skip pytest)
 set -o pipefail
-TAG=${1:-r3}
+TAG=${1:-rec}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
