@@ -562,7 +562,7 @@ def coop_roofline(L, cg, avg, calls, bodies: int, iter_bytes: int) -> dict:
     ach = iter_bytes / t_body / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": f"k_cg_coop_{'tg' if T.value else 'wt'}",
+            "kernel": f"k_cg_coop_{'st' if T.value == 2 else 'wt'}",
             "template": f"<{R.value}, {NT.value}>", "workgroups": G.value,
             "bytes_per_launch": int(iter_bytes * bodies / max(calls[1], 1)),
             "bytes_basis": "compulsory bytes of a body as the three-kernel body moves them "

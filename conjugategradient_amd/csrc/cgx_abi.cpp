@@ -170,14 +170,10 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
     // boundary slices (or wait, then one launch when the matrix is not split).
     // A split SELL matrix carries the push in the interior launch's first
     // workgroups (k_spmv_dot_push: the xGMI stores overlap the interior
-    // slices, one launch less; $CGX_PEER_PUSH_MERGE=0 keeps k_peer_push)
+    // slices, one launch less)
     const bool split = A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192));
     const int wg0 = A->peer.dev.nsend * kPushWG;
-    static const bool merge_on = [] {
-      const char *e = std::getenv("CGX_PEER_PUSH_MERGE");
-      return !e || std::atoi(e) != 0;
-    }();
-    const bool merged = split && wg0 > 0 && merge_on && Launch<T>::push_supported(A->dev);
+    const bool merged = split && wg0 > 0 && Launch<T>::push_supported(A->dev);
     // (the wait stays a launch of its own: round 2's folded form had the
     // boundary workgroups spin on flags raised by the same launch's first
     // workgroups, which relies on their being resident; removed in round 3,
@@ -188,12 +184,9 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
                             : Launch<T>::slice_grid(A->dev, A->split_ni);
     // the boundary slices wait for the neighbours' pushes themselves and read
     // the ghosts from the landing buffer (k_spmv_dot_bnd): no k_peer_wait
-    // launch, no copy into p's ghost tail; $CGX_PEER_WAIT_FOLD=0 keeps them
-    static const bool fold_on = [] {
-      const char *e = std::getenv("CGX_PEER_WAIT_FOLD");
-      return !e || std::atoi(e) != 0;
-    }();
-    const bool fold = split && A->split_nb > 0 && fold_on && Launch<T>::bnd_supported(A->dev);
+    // launch, no copy into p's ghost tail (matrices without the split keep
+    // k_peer_wait before their one launch)
+    const bool fold = split && A->split_nb > 0 && Launch<T>::bnd_supported(A->dev);
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = hipSuccess;
            if (merged)
@@ -258,13 +251,9 @@ int dist_dot(cgx_cg *cg, const T *part, int np, T *dst, int slot, int which) {
 // The device peer transport's two all-reduces of a body run inside the
 // kernels that consume them (update_r: p.Ap, the x/p update: r.r; every
 // workgroup polls the mailboxes, peerdev::world_sum) instead of as two
-// one-workgroup launches; $CGX_PEER_AR_FUSE=0 keeps k_peer_allreduce.
+// one-workgroup launches (k_peer_allreduce, round 2's form).
 static const PeerDev *fused_ar(const cgx_cg *cg) {
-  static const bool on = [] {
-    const char *e = std::getenv("CGX_PEER_AR_FUSE");
-    return !e || std::atoi(e) != 0;
-  }();
-  return (on && cg->A->dist && cg->A->peer.on) ? &cg->A->peer.dev : nullptr;
+  return (cg->A->dist && cg->A->peer.on) ? &cg->A->peer.dev : nullptr;
 }
 
 template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
@@ -395,24 +384,14 @@ int enqueue_coop(cgx_cg *cg, int slot, int64_t bodies) {
   const CsrDev &A = cg->A->dev;
   const int m = (int)std::min<int64_t>(bodies, 1 << 30);
   return timed(cg, 1, cg->ctx->stream, [&] {
-    return cg_coop(cg->n, cg->coop_r, cg->coop_stream ? 1024 : cg->coop_nt,
-                   cg->coop_stream ? 2 : cg->coop_tagr ? 1 : 0, A.rowptr, A.col, (const double *)A.val,
+    return cg_coop(cg->n, cg->coop_r, cg->coop_stream, A.rowptr, A.col, (const double *)A.val,
                    (double *)cg->x, (double *)cg->r, (double *)cg->p, (double *)cg->p2,
-                   (unsigned long long *)cg->coop_rg, (CgScalars<double> *)cg->st, slot, m,
-                   (CoopWs *)cg->coop_ws, cg->coop_ticks,
-                   (unsigned long long *)cg->coop_trace, cg->coop_nap, cg->coop_stall,
-                   cg->ctx->stream);
+                   (CgScalars<double> *)cg->st, slot, m, (CoopWs *)cg->coop_ws, cg->coop_ticks,
+                   (unsigned long long *)cg->coop_trace, cg->coop_stall, cg->ctx->stream);
   });
 }
 
-// $CGX_COOP_REG_MAXG: workgroups of mode 5's register forms (A/B; default
-// kCoopMaxGReg)
-int coop_reg_maxg() {
-  const char *e = std::getenv("CGX_COOP_REG_MAXG");
-  return e ? std::max(1, std::atoi(e)) : kCoopMaxGReg;
-}
-
-// $CGX_COOP_R: mode 5's rows per thread (1, 2, 4; unset: the fewest that fit)
+// $CGX_COOP_R: the streamed form's rows per thread (unset: the fewest that fit)
 int coop_want_r() {
   const char *e = std::getenv("CGX_COOP_R");
   return e ? std::atoi(e) : 0;
@@ -702,15 +681,11 @@ extern "C" int cgx_free(cgx_ctx *ctx, void *d) {
 // solution, a CSR download) go through a ring of two pinned 64 MiB chunks:
 // the DMA engine fills chunk k+1 while several host threads copy chunk k out
 // (15-17 GB/s against 10 for one hipMemcpy, profiles/r01_setup.json). Small
-// copies, and $CGX_STAGED=0, use one hipMemcpyAsync.
+// copies use one hipMemcpyAsync.
 constexpr size_t kStageChunk = size_t(64) << 20;
 constexpr size_t kStageMin = size_t(16) << 20;
 
-static bool staged(size_t bytes) {
-  if (bytes < kStageMin) return false;
-  const char *e = std::getenv("CGX_STAGED");
-  return !(e && std::atoi(e) == 0);
-}
+static bool staged(size_t bytes) { return bytes >= kStageMin; }
 
 static int ensure_stage(cgx_ctx *ctx) {
   for (int b = 0; b < 2; ++b) {
@@ -1014,7 +989,6 @@ void free_sell(cgx_csr *A) {
   A->dev.sell_maxw = 0;
   A->dev.march_k = A->dev.march_a = A->dev.march_len = 0;
   A->dev.march_pat = -1;
-  A->dev.ymarch_k = A->dev.ymarch_a = 0;
   A->sell_padded = 0;
   A->sell_idx_words = 0;
   A->vc_chunks = 0;
@@ -1155,14 +1129,10 @@ static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
 // 7-point) or {-D, -1, 0, 1, D} (2-D 5-point) with D a positive multiple of
 // the 128-row slice and 1 < a < D. Slices with another pattern (or the same
 // pattern at another pool base) still run, through the per-slice form.
-// $CGX_MARCH=0 turns it off, $CGX_MARCH_LEN sets planes per run (A/B).
 static void plan_march(const std::vector<SellSlice> &sl, const std::vector<int> &pool,
                        int64_t nx, size_t es, CsrDev &dev) {
   dev.march_k = dev.march_a = dev.march_len = 0;
   dev.march_pat = -1;
-  dev.ymarch_k = dev.ymarch_a = 0;
-  if (const char *e = std::getenv("CGX_MARCH"))
-    if (std::atoi(e) == 0) return;
   if (sl.empty() || (uint64_t)nx * es >= (uint64_t(1) << 32)) return;
   std::map<std::pair<int, int>, int64_t> freq;  // (pool base, width) -> slices
   for (const SellSlice &m : sl) ++freq[{m.dict, m.width}];
@@ -1184,14 +1154,6 @@ static void plan_march(const std::vector<SellSlice> &sl, const std::vector<int> 
   dev.march_k = D / H;
   dev.march_a = a;
   dev.march_pat = base;
-  // the y-march of a 3-D pattern: lines of a = nx rows, a whole number of
-  // slices; the gathered offset is D
-  dev.ymarch_k = dev.ymarch_a = 0;
-  if (W == 7 && a % H == 0) {
-    dev.ymarch_k = a / H;
-    dev.ymarch_a = D;
-  }
-  if (const char *e = std::getenv("CGX_MARCH_LEN")) dev.march_len = std::max(0, std::atoi(e));
 }
 
 extern "C" int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
@@ -1275,8 +1237,6 @@ extern "C" int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, i
 // kernel's sell_range splits a list. Empty when no reordering applies.
 std::vector<int> chunked_slice_order(const std::vector<int> &ids, int64_t H, int64_t P,
                                      int64_t kChunk) {
-  if (const char *env = std::getenv("CGX_SELL_ORDER_CHUNK"))  // A/B knob
-    kChunk = std::max<int64_t>(1, std::atoll(env));
   std::vector<int> order;
   if (P / H < 2 * kChunk) return order;
   const int64_t m = (int64_t)ids.size();
@@ -1744,12 +1704,6 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   if (R == 0) {
     R = 3;
     fallback = true;
-    if (const char *env = std::getenv("CGX_SELL")) {
-      R = std::atoi(env);
-      if (R == 0) return CGX_OK;
-      if (R < 1 || R > 3) R = 3;
-      fallback = R == 3;
-    }
   }
   free_sell(A);
   const int64_t n = A->dev.n, nnz = A->dev.nnz;
@@ -1813,19 +1767,14 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   // least two chunks of 512 slices (the XCD's ~1,024 slices in flight then
   // hold every +-plane gather in its L2: 512^3 SpMV 793 -> 710 us, the
   // iteration 463 -> 483 it/s; profiles/r03m_order_chunk.log). 256^3
-  // planes (512 slices) keep the natural order, which is the same walk.
-  // $CGX_SELL_ORDER=1 forces it with chunks of 128 slices (the round-2
-  // form, no faster at 256^3: DESIGN.md §8), =0 turns it off.
+  // planes (512 slices) keep the natural order, which is the same walk
+  // (chunks of 128 slices, round 2's form, were no faster at 256^3: DESIGN.md
+  // §8).
   {
     int64_t P = 0;
     for (int v : pool) P = std::max<int64_t>(P, v < 0 ? -(int64_t)v : v);
-    const char *env = std::getenv("CGX_SELL_ORDER");
-    const int req = env ? std::atoi(env) : -1;
     std::vector<int> order;
-    if (req == 1)
-      order = sell_visit_order(nsl, (int64_t)kSellRows * R, P, 128);
-    else if (req < 0 && !A->dist)
-      order = sell_visit_order(nsl, (int64_t)kSellRows * R, P, 512);
+    if (!A->dist) order = sell_visit_order(nsl, (int64_t)kSellRows * R, P, 512);
     if (!order.empty()) {
       e = hipMalloc(&A->d_sell_order, order.size() * sizeof(int));
       if (e == hipSuccess)
@@ -1970,19 +1919,19 @@ extern "C" int cgx_csr_sell_info(cgx_csr *A, int *has_sell, int64_t *padded) {
   return CGX_OK;
 }
 
+// A request names a form k_spmv_dot is instantiated for (CGX_SPMV_LIST,
+// the forms cgx_csr_variant reports) or one of the request forms below,
+// which resolve to such a form on a matrix with the right copies (the
+// checks in cgx_csr_set_variant); the lean walk is handled before this.
 static bool known_variant(int v) {
   static const int ok[] = {0,  1,  2,  3,  4,  5,  6,  7,  12, 13, 14, 15, 133, 135, 264, 265, 266,
                            267, 2048, 2050, 2056, 2058, 6144, 6146, 8192, 8194, 24576, 24578,
                            34816, 34818, 40960, 40962, 296960, 296962, 559104, 559106,
                            821248, 821250, 1607680, 1607682, 1869824, 1869826,
-                           9209856, 9209858, 10258432, 10258434, 12355584, 12355586};
+                           9209856, 9209858, 10258434, 12355584, 12355586, 10258432};
   for (int k : ok)
     if (k == v) return true;
-  // the resolved SELL-P forms cgx_csr_variant reports (e.g. 1875970) are
-  // accepted back as requests
-  constexpr int sellp_bits = 8192 | 16384 | 32768 | 65536 | 131072 | 262144 | 524288 | 1048576 |
-                             2097152 | kVT | kYM | 2;
-  return (v & 8192) && !(v & ~sellp_bits);
+  return spmv_listed(v);
 }
 
 extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
@@ -2096,14 +2045,12 @@ int autotune_spmv(cgx_csr *A) {
   // 1048576: one gather pair fewer per offset -1 / +1)
   for (int c4 : {0, 262144}) {
     if (!A->dev.svc || (c4 && !A->dev.svc4)) continue;
-    // (the y-march forms, kYM, measured 93-124 us against 72 for the
-    // templated consecutive walk at 256^3: reachable by request only,
-    // profiles/r03_ymarch_tune.log)
+    // (a y-march form measured 93-124 us against 72 for the templated
+    // consecutive walk at 256^3, profiles/r03_ymarch_tune.log: removed)
     for (int pipe : {0, 524288, 524288 | 1048576, 524288 | 1048576 | 2097152,
                      524288 | kVT, 524288 | 1048576 | kVT, 524288 | 1048576 | 2097152 | kVT}) {
       if (pipe && A->dev.sell_maxw > 8) continue;
       if ((pipe & 2097152) && A->dev.march_k < 1) continue;
-      if ((pipe & kYM) && (!c4 || A->dev.ymarch_k < 1)) continue;  // 4-bit forms only
       if ((pipe & kVT) && (!c4 || !A->dev.sl_t)) continue;
       if (!big) cands.push_back(2048 | 32768 | c4 | pipe);
       cands.push_back(2050 | 32768 | c4 | pipe);
@@ -2406,9 +2353,8 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
     return hip_fail(e, "cgx_cg_create");
   }
   cg->fused = false;
-  // alternating sweep directions: +0.5-2% at 256^3; $CGX_ALTDIR=0 off
+  // alternating sweep directions: +0.5-2% at 256^3
   cg->altdir = true;
-  if (const char *e = std::getenv("CGX_ALTDIR")) cg->altdir = std::atoi(e) != 0;
   *out = cg;
   // auto mode: the x update deferred over four p buffers, in three kernels
   // (mode 3: +4-8% over mode 1 at 256^3) or, where it pays,
@@ -2430,7 +2376,6 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
 static bool fd_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
   if (A->dist || cg->dtype != CGX_F64 || !Launch<double>::fd_supported(A->dev)) return false;
-  if (const char *e = std::getenv("CGX_AUTO_FD")) return std::atoi(e) != 0;  // A/B
   const int v = launch_variant(A->dev, cg->dtype);
   const bool march2d = (v & 2097152) && A->dev.march_a == 0;
   const bool small = A->dev.nnz * (int64_t)(sizeof(double) + sizeof(int)) < (int64_t(64) << 20);
@@ -2456,7 +2401,7 @@ static int device_cus(const cgx_cg *cg) {
 }
 static bool coop_fits(const cgx_cg *cg, int R) {
   if (R <= 0) return false;
-  const int64_t per = (int64_t)cg->coop_nt * R;
+  const int64_t per = (int64_t)1024 * R;
   return (cg->n + per - 1) / per <= device_cus(cg);
 }
 // The streamed form (2): rows of any length, R <= 8 rows per thread of
@@ -2465,7 +2410,7 @@ static int coop_stream_r(const cgx_cg *cg) {
   return coop_stream_rows(cg->n, coop_want_r(), device_cus(cg));
 }
 // auto: where neither register form applies (rows past 7 entries, or past
-// kCoopMaxGReg workgroups), the matrix is on the CSR-stream path (it has no
+// kCoopMaxG workgroups), the matrix is on the CSR-stream path (it has no
 // SELL copy: the stencils' SELL-P / value-code bodies win there) and the
 // streamed form fits with at most kCoopStreamAutoR rows per thread — where
 // it was measured to win (profiles/r03_coop_stream.log: irregular 100k /
@@ -2477,7 +2422,6 @@ constexpr int kCoopStreamAutoR = 2;
 static bool coop_stream_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
   if (A->dist || cg->dtype != CGX_F64 || cg->coop_stream_want == 0) return false;
-  if (const char *e = std::getenv("CGX_AUTO_COOP"); e && std::atoi(e) == 0) return false;
   const int R = coop_stream_r(cg);
   if (R <= 0) return false;
   if (cg->coop_stream_want == 1) return true;
@@ -2487,13 +2431,8 @@ static bool coop_stream_auto(const cgx_cg *cg) {
 static bool coop_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
   if (A->dist || cg->dtype != CGX_F64) return false;
-  if (const char *e = std::getenv("CGX_AUTO_COOP")) {
-    if (std::atoi(e) == 0) return false;
-  }
   // rows whose entries all sit in registers (7 in the 1,024-thread form)
-  const int kc = cg->coop_nt == 1024 ? 7 : kCoopK;
-  return A->max_row_nnz <= kc && coop_rows_per_thread(cg->n, 1, cg->coop_nt, coop_reg_maxg()) == 1 &&
-         coop_fits(cg, 1);
+  return A->max_row_nnz <= 7 && coop_rows_per_thread(cg->n, kCoopMaxG) == 1 && coop_fits(cg, 1);
 }
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
@@ -2502,13 +2441,7 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
               "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
               "4 fused with deferred x, 5 persistent body", mode);
   int coop_r = 0;
-  if (!cg->begun) {  // mode 5's shape knobs (A/B; the defaults are the measured best)
-    cg->coop_nt = 1024;
-    cg->coop_nap = 1;
-    cg->coop_tagr = false;
-    if (const char *e = std::getenv("CGX_COOP_NT")) cg->coop_nt = std::atoi(e);
-    if (const char *e = std::getenv("CGX_COOP_NAP")) cg->coop_nap = std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("CGX_COOP_TAGR")) cg->coop_tagr = std::atoi(e) != 0;
+  if (!cg->begun) {  // mode 5's form and test hook
     cg->coop_stall = -1;
     if (const char *e = std::getenv("CGX_COOP_INJECT_STALL")) cg->coop_stall = std::atoi(e);
     cg->coop_stream_want = -1;
@@ -2522,12 +2455,11 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     // tails per thread from the CSR arrays in the register forms: the
     // streamed form is faster there (irregular 100k rows: 11.2 against 15.0
     // us per body, profiles/r03_coop_stream*.log) and is taken when it fits
-    const int kc = cg->coop_nt == 1024 ? 7 : kCoopK;
     const bool prefer_stream =
         cg->coop_stream_want == 1 ||
-        (cg->coop_stream_want != 0 && cg->A->max_row_nnz > kc && coop_stream_r(cg) > 0);
+        (cg->coop_stream_want != 0 && cg->A->max_row_nnz > 7 && coop_stream_r(cg) > 0);
     if (!prefer_stream) {
-      coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt, coop_reg_maxg());
+      coop_r = coop_rows_per_thread(cg->n, kCoopMaxG);
       if (coop_r > 0 && !coop_fits(cg, coop_r)) coop_r = 0;
     }
     if (coop_r == 0 && cg->coop_stream_want != 0) {
@@ -2551,7 +2483,7 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
   if (mode == 0) {
     mode = coop_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
-    if (mode == 5) coop_r = coop_rows_per_thread(cg->n, coop_want_r(), cg->coop_nt, coop_reg_maxg());
+    if (mode == 5) coop_r = coop_rows_per_thread(cg->n, kCoopMaxG);
     if (mode != 5 || coop_r == 0) {
       mode = coop_stream_auto(cg) ? 5 : fd_auto(cg) ? 4 : 3;
       if (mode == 5) {
@@ -2580,10 +2512,6 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     cg->coop_ticks = (long long)clk_khz * 1000 * 2;  // 2 s: a resident grid never waits so long
     if (const char *e = std::getenv("CGX_COOP_TIMEOUT_MS"))
       cg->coop_ticks = (long long)clk_khz * std::max(1, std::atoi(e));
-  }
-  if (c && cg->coop_tagr && !stream && !cg->coop_rg) {  // the tagged form's p / r granules
-    DeviceGuard g(cg->ctx->device);
-    CGX_HIP(hipMalloc(&cg->coop_rg, (size_t)cg->n * 48));
   }
   cg->coop = c;
   if (c) {
@@ -2637,7 +2565,7 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   drop_graph(cg);
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
   for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2],
-                  cg->coop_ws, cg->coop_rg, cg->coop_trace})
+                  cg->coop_ws, cg->coop_trace})
     if (p) (void)hipFree(p);
   cgx_csr *A = cg->A;
   cgx_ctx *ctx = cg->ctx;
@@ -2857,15 +2785,15 @@ extern "C" int cgx_cg_prepare(cgx_cg *cg, int64_t bodies) {
 }
 
 extern "C" int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads,
-                                 int *workgroups, int *tagged) {
-  CGX_REQUIRE(cg && rows_per_thread && threads && workgroups && tagged, CGX_EINVAL,
+                                 int *workgroups, int *form) {
+  CGX_REQUIRE(cg && rows_per_thread && threads && workgroups && form, CGX_EINVAL,
               "NULL argument");
   CGX_REQUIRE(cg->coop, CGX_ESTATE, "the solver is not in mode 5");
   *rows_per_thread = cg->coop_r;
-  *threads = cg->coop_stream ? 1024 : cg->coop_nt;
+  *threads = 1024;
   const int64_t per = (int64_t)*threads * cg->coop_r;
   *workgroups = (int)((cg->n + per - 1) / per);
-  *tagged = cg->coop_stream ? 2 : cg->coop_tagr ? 1 : 0;
+  *form = cg->coop_stream ? 2 : 0;
   return CGX_OK;
 }
 

@@ -7,10 +7,12 @@
 // mostly kernel boundaries (128^2: ~9.6 us per body, of which the work is a
 // fraction), this body pays two grid-wide exchanges instead.
 //
-// Layout: workgroup g owns rows [g 256 R, (g + 1) 256 R), thread t rows
-// g 256 R + 256 u + t (u < R). Each thread keeps its rows' x, r, p and the
-// first kCoopK entries of each row (columns and values) in registers for the
-// whole launch; the rest of a longer row is read from the CSR arrays.
+// Layout (the register form): workgroup g of 1,024 threads owns rows
+// [1024 g, 1024 (g + 1)), one per thread. Each thread keeps its row's x, r,
+// p and its first 7 entries (columns and values) in registers for the whole
+// launch; the rest of a longer row is read from the CSR arrays. (Round 3's
+// 256- and 512-thread shapes and its tagged p / r hand-off measured no faster
+// and were removed in round 4.)
 //
 // Per body k (two exchanges, DESIGN.md §5 "persistent body"):
 //   1. SpMV on p_k. p_k[j] of a gathered column is formed where it is read,
@@ -165,37 +167,6 @@ __device__ __forceinline__ bool collect(const unsigned long long *gran, unsigned
 
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// One entry of a tagged vector copy: two {tag, half} granules per entry,
-// each written by one 8-byte atomic store (the data is the flag, MI355X guide
-// §6 Guideline 16 R2). ld_tagged re-reads until both halves carry `tag`
-// (bounded; on timeout it raises tmo and returns 0).
-__device__ __forceinline__ void st_tagged(unsigned long long *g, int64_t j, double v,
-                                          unsigned tag) {
-  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-  const unsigned long long hi = (unsigned long long)tag << 32;
-  st_ag(g + 2 * j, hi | (u & 0xffffffffull));
-  st_ag(g + 2 * j + 1, hi | (u >> 32));
-}
-__device__ __forceinline__ double untag(unsigned long long a, unsigned long long b) {
-  return __longlong_as_double((long long)((a & 0xffffffffull) | ((b & 0xffffffffull) << 32)));
-}
-__device__ __forceinline__ bool tagged(unsigned long long a, unsigned long long b, unsigned tag) {
-  return (unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag;
-}
-__device__ __forceinline__ double ld_tagged(const unsigned long long *g, int64_t j, unsigned tag,
-                                            long long t0, long long ticks, unsigned *tmo) {
-  for (;;) {
-    const unsigned long long a = ld_ag(g + 2 * j), b = ld_ag(g + 2 * j + 1);
-    if (tagged(a, b, tag)) return untag(a, b);
-    if (wall_clock64() - t0 > ticks ||
-        __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return 0.0;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // Diagnostics ($CGX_COOP_TRACE, cgx_cg_coop_trace): thread 0 of every
 // workgroup stamps the wall clock at the phases of bodies 8-15 of a launch
 #define CGX_COOP_TR(ph)                                                                  \
@@ -265,7 +236,7 @@ __device__ __forceinline__ void coop_gave_up(CgScalars<double> *st) {
   }
 }
 
-// Form 0 (write-through, $CGX_COOP_TAGR=0): r and p_k stored with agent-scope
+// The register form: r and p_k stored with agent-scope
 // stores (sc1) into r and p0 / p1, every storing wave drained before its
 // workgroup publishes; the gathers of a body run after both exchanges.
 template <int R, int NT>
@@ -365,152 +336,18 @@ __global__ __launch_bounds__(NT, 1) void k_cg_coop_wt(
   coop_gave_up(st);
 }
 
-// Form 1 (tagged, the default): p_k and r_{k+1} are handed over as tagged
-// granules (pg: two copies of 2 n words, body k in copy k mod 2; rg: 2 n
-// words; all zeroed before the launch), so no exchange waits for a drain,
-// and the next body's gathers are issued right after this body's r.r
-// partial is published: they overlap the r.r exchange (a gatherer that
-// finds a stale tag re-reads, bounded). Same values as form 0.
-template <int R, int NT>
-__global__ __launch_bounds__(NT, 1) void k_cg_coop_tg(
-    int64_t n, const int *__restrict__ rowptr, const int *__restrict__ col,
-    const double *__restrict__ val, double *__restrict__ x, double *r, double *p0,
-    unsigned long long *pg, unsigned long long *rg, CgScalars<double> *st, int slot0, int m,
-    CoopWs *cw, long long ticks, unsigned long long *trace, int nap, int stall) {
-  CGX_COOP_PROLOGUE
-  double gp[R][KC], gr[R][KC];  // this body's gathered p_{k-1}[j] (body 0: p_k) and r_k[j]
-#pragma unroll
-  for (int u = 0; u < R; ++u)
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      gp[u][k] = k < cnt[u] ? ld_ag(p0 + cc[u][k]) : 0.0;
-      gr[u][k] = 0.0;
-    }
-  double beta = 0.0;
-  for (int i = 0; i < m; ++i) {
-    const int s = (slot0 + i) & 3;
-    const unsigned tag = (unsigned)i + 1u;
-    CGX_COOP_TR(0)
-    unsigned long long *pgc = pg + (size_t)(i & 1) * 2 * n;  // p_k, tag i + 1
-    const unsigned long long *pgp = pg + (size_t)((i + 1) & 1) * 2 * n;  // p_{k-1}, tag i
-    double q[R];
-    if (i > 0) {
-#pragma unroll
-      for (int u = 0; u < R; ++u) pv[u] = rv[u] + beta * pv[u];  // CG.hpp:418, own rows
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (row[u] < n) st_tagged(pgc, row[u], pv[u], tag);
-    const long long t0 = wall_clock64();
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      double acc = 0.0;
-      if (i == 0) {
-#pragma unroll
-        for (int k = 0; k < KC; ++k)
-          if (k < cnt[u]) acc += cv[u][k] * gp[u][k];
-        for (int k = KC; k < cnt[u]; ++k) acc += val[rb[u] + k] * ld_ag(p0 + col[rb[u] + k]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < KC; ++k)
-          if (k < cnt[u]) acc += cv[u][k] * (gr[u][k] + beta * gp[u][k]);
-        for (int k = KC; k < cnt[u]; ++k) {
-          const int j = col[rb[u] + k];
-          acc += val[rb[u] + k] * (ld_tagged(rg, j, (unsigned)i, t0, ticks, &cw->tmo) +
-                                   beta * ld_tagged(pgp, j, (unsigned)i, t0, ticks, &cw->tmo));
-        }
-      }
-      q[u] = acc;
-    }
-    CGX_COOP_TR(1)
-    // p.Ap (CG.hpp:374-379)
-    double part = 0.0;
-#pragma unroll
-    for (int u = 0; u < R; ++u) part += pv[u] * q[u];
-    part = block_sum<NT>(part, red[0]);
-    CGX_COOP_TR(2)
-    // fault injection (tests): workgroup 0 withholds body `stall`'s p.Ap
-    // partial, so every other workgroup's bounded spin gives up
-    if (!(i == stall && blockIdx.x == 0)) publish(cw->ga, part, tag);
-    if (!collect(cw->ga, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
-    CGX_COOP_TR(3)
-    const double pAp = res;
-    const double alpha = rxr / pAp;
-    // x += alpha p; r -= alpha Ap; r.r   (CG.hpp:381-393, 406-407)
-    part = 0.0;
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      xr[u] = xr[u] + alpha * pv[u];
-      rv[u] = rv[u] - alpha * q[u];
-      if (row[u] < n) st_tagged(rg, row[u], rv[u], tag);
-      part += rv[u] * rv[u];
-    }
-    part = block_sum<NT>(part, red[1]);
-    CGX_COOP_TR(4)
-    publish(cw->gb, part, tag);
-    if (i < m - 1) {
-      // the next body's gathers: p_k[j] (tag i + 1, stored above by every
-      // workgroup) and r_{k+1}[j] (tag i + 1, stored after the p.Ap exchange)
-      const long long t1 = wall_clock64();
-      bool bad = false;
-#pragma unroll
-      for (int u = 0; u < R; ++u)
-#pragma unroll
-        for (int k = 0; k < KC; ++k)
-          if (k < cnt[u]) {
-            const int j = cc[u][k];
-            const unsigned long long a = ld_ag(pgc + 2 * j), b = ld_ag(pgc + 2 * j + 1);
-            const unsigned long long c = ld_ag(rg + 2 * j), d = ld_ag(rg + 2 * j + 1);
-            bad |= !tagged(a, b, tag) || !tagged(c, d, tag);
-            gp[u][k] = untag(a, b);
-            gr[u][k] = untag(c, d);
-          }
-      if (__any(bad)) {  // stores not landed yet: re-read until they have
-#pragma unroll
-        for (int u = 0; u < R; ++u)
-#pragma unroll
-          for (int k = 0; k < KC; ++k)
-            if (k < cnt[u]) {
-              gp[u][k] = ld_tagged(pgc, cc[u][k], tag, t1, ticks, &cw->tmo);
-              gr[u][k] = ld_tagged(rg, cc[u][k], tag, t1, ticks, &cw->tmo);
-            }
-      }
-    }
-    CGX_COOP_TR(5)
-    if (!collect(cw->gb, tag, ticks, &cw->tmo, &res, &okf, nap)) break;
-    CGX_COOP_TR(6)
-    const double rr = res;
-    ++bodies;
-    const bool cont = coop_record(st, s, pAp, rr, alpha, rxr, tol, bodies, cap);
-    beta = rr / rxr;
-    rxr = rr;
-    if (!cont || i == m - 1) {
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        if (row[u] < n) {
-          p0[row[u]] = rv[u] + beta * pv[u];  // p_{k+1}, x and r in the standard buffers
-          x[row[u]] = xr[u];
-          r[row[u]] = rv[u];
-        }
-      }
-      return;
-    }
-  }
-  coop_gave_up(st);
-}
-
 // Form 2 (streamed, problems past the register forms: more rows than
-// kCoopMaxGReg x 1,024, or rows longer than 7 entries): 1,024 threads, R rows
+// kCoopMaxG x 1,024, or rows longer than 7 entries): 1,024 threads, R rows
 // per thread, r of the rows in registers, x and p in LDS (the 128-VGPR
 // budget of 16 waves per CU), the matrix read every body. Chunk u of
 // workgroup g is rows [(g R + u) 1024, + 1024), whose entries are
 // contiguous: the workgroup's threads load them coalesced (entry e by thread
 // e mod 1024, four per pass in flight), form each product
-// val[e] * p_k[col[e]] (p_k[j] = r_k[j] + beta p_{k-1}[j], as form 0) and
+// val[e] * p_k[col[e]] (p_k[j] = r_k[j] + beta p_{k-1}[j], as the register form) and
 // stage it in LDS; thread t then sums its row's products in ascending entry
 // order from 0 — the reference's row loop, bit for bit. A chunk of more than
 // coop_stage<R>() entries (long rows) is summed by its row threads from the
-// CSR arrays instead. Exchanges, updates and the record as form 0.
+// CSR arrays instead. Exchanges, updates and the record as the register form.
 constexpr int kCoopStP = 5;  // streamed form: entries per thread of a one-pass chunk
 template <int R> constexpr int coop_stage() { return (160 * 1024 - R * 1024 * 16 - 1024) / 8; }
 template <int R>
@@ -698,16 +535,9 @@ __global__ __launch_bounds__(1024, 1) void k_cg_coop_st(
 
 }  // namespace
 
-int coop_rows_per_thread(int64_t n, int want, int nt, int max_g) {
-  static const int opts[] = {1, 2, 4};
-  if (nt != 256 && nt != 512 && nt != 1024) return 0;
-  for (int R : opts) {
-    if (want > 0 && R != want) continue;
-    if (nt == 1024 && R != 1) continue;  // 128 VGPRs at 16 waves per CU
-    if (nt == 512 && R > 2) continue;    // <4, 512> spills
-    if ((n + (int64_t)nt * R - 1) / ((int64_t)nt * R) <= std::min(max_g, kCoopMaxG)) return R;
-  }
-  return 0;
+int coop_rows_per_thread(int64_t n, int max_g) {
+  // one row per thread of 1,024 (128 VGPRs at 16 waves per CU)
+  return (n + 1023) / 1024 <= std::min(max_g, kCoopMaxG) ? 1 : 0;
 }
 
 int coop_stream_rows(int64_t n, int want, int max_g) {
@@ -738,62 +568,36 @@ static bool coop_resident(const void *fn, int NT, int G) {
   return G <= it->second;
 }
 
-hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const int *col,
+hipError_t cg_coop(int64_t n, int R, bool streamed, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
-                   unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
-                   long long ticks, unsigned long long *trace, int nap, int stall,
-                   hipStream_t s) {
+                   CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks,
+                   unsigned long long *trace, int stall, hipStream_t s) {
+  constexpr int NT = 1024, nap = 1;  // one s_sleep(1) per exchange poll
   const int G = (int)((n + (int64_t)NT * R - 1) / ((int64_t)NT * R));
-  const bool tagged = form == 1;
-  if (G < 1 || G > kCoopMaxG || m < 1 || (tagged && !g)) return hipErrorInvalidValue;
-  if (form == 2 && (NT != 1024 || R < 1 || R > kCoopStreamMaxR)) return hipErrorInvalidValue;
-
+  if (G < 1 || G > kCoopMaxG || m < 1) return hipErrorInvalidValue;
+  if (streamed ? (R < 1 || R > kCoopStreamMaxR) : R != 1) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
-  if (e == hipSuccess && tagged) e = hipMemsetAsync(g, 0, (size_t)n * 48, s);
   if (e != hipSuccess) return e;
-  unsigned long long *pg = g, *rg = g ? g + 4 * n : nullptr;
-#define CGX_COOP_FIT(K, TT) \
-  if (!coop_resident((const void *)K, TT, G)) return hipErrorCooperativeLaunchTooLarge
-#define CGX_COOP_WT(RR, TT)                                                                 \
-  CGX_COOP_FIT((k_cg_coop_wt<RR, TT>), TT);                                                 \
-  k_cg_coop_wt<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
-                                        ticks, trace, nap, stall)
-#define CGX_COOP_TG(RR, TT)                                                                 \
-  CGX_COOP_FIT((k_cg_coop_tg<RR, TT>), TT);                                                 \
-  k_cg_coop_tg<RR, TT><<<G, TT, 0, s>>>(n, rowptr, col, val, x, r, p0, pg, rg, st, slot0, m, \
-                                        cw, ticks, trace, nap, stall)
-#define CGX_COOP_ST(RR)                                                                     \
-  case RR:                                                                                  \
-    CGX_COOP_FIT(k_cg_coop_st<RR>, 1024);                                                   \
-    k_cg_coop_st<RR><<<G, 1024, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw, \
-                                        ticks, trace, nap, stall);                          \
-    break;
-  if (form == 2) {
-    switch (R) {
-      CGX_COOP_ST(1) CGX_COOP_ST(2) CGX_COOP_ST(3) CGX_COOP_ST(4)
-      CGX_COOP_ST(5) CGX_COOP_ST(6) CGX_COOP_ST(7) CGX_COOP_ST(8)
-      default: return hipErrorInvalidValue;
-    }
-#undef CGX_COOP_ST
+#define CGX_COOP_FIT(K) \
+  if (!coop_resident((const void *)K, NT, G)) return hipErrorCooperativeLaunchTooLarge
+  if (!streamed) {
+    CGX_COOP_FIT((k_cg_coop_wt<1, NT>));
+    k_cg_coop_wt<1, NT><<<G, NT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw,
+                                         ticks, trace, nap, stall);
     return hipGetLastError();
   }
-  const int key = (NT == 1024 ? 100 : NT == 512 ? 50 : 0) + R * 2 + (tagged ? 1 : 0);
-  switch (key) {
-    case 2: CGX_COOP_WT(1, 256); break;
-    case 3: CGX_COOP_TG(1, 256); break;
-    case 4: CGX_COOP_WT(2, 256); break;
-    case 5: CGX_COOP_TG(2, 256); break;
-    case 8: CGX_COOP_WT(4, 256); break;
-    case 9: CGX_COOP_TG(4, 256); break;
-    case 52: CGX_COOP_WT(1, 512); break;
-    case 53: CGX_COOP_TG(1, 512); break;
-    case 54: CGX_COOP_WT(2, 512); break;
-    case 102: CGX_COOP_WT(1, 1024); break;
-    case 103: CGX_COOP_TG(1, 1024); break;
+#define CGX_COOP_ST(RR)                                                                     \
+  case RR:                                                                                  \
+    CGX_COOP_FIT(k_cg_coop_st<RR>);                                                         \
+    k_cg_coop_st<RR><<<G, NT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw,   \
+                                      ticks, trace, nap, stall);                            \
+    break;
+  switch (R) {
+    CGX_COOP_ST(1) CGX_COOP_ST(2) CGX_COOP_ST(3) CGX_COOP_ST(4)
+    CGX_COOP_ST(5) CGX_COOP_ST(6) CGX_COOP_ST(7) CGX_COOP_ST(8)
     default: return hipErrorInvalidValue;
   }
-#undef CGX_COOP_WT
-#undef CGX_COOP_TG
+#undef CGX_COOP_ST
 #undef CGX_COOP_FIT
   return hipGetLastError();
 }

@@ -629,17 +629,15 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     // the interior slices in the chunked visit order of a single-device
     // matrix (cgx_abi.cpp build_sell), planed by the farthest local band
     // (ghost columns excluded): the 512x512x64 slab's planes span 2,048
-    // slices, as 512^3's do; $CGX_SELL_ORDER as there
-    const char *oenv = std::getenv("CGX_SELL_ORDER");
-    const int oreq = oenv ? std::atoi(oenv) : -1;
-    if (!in.empty() && !bd.empty() && oreq != 0) {
+    // slices, as 512^3's do
+    if (!in.empty() && !bd.empty()) {
       int64_t P = 0;
       for (int64_t r = 0; r < n_local; ++r)
         for (int64_t k = hrp[(size_t)r]; k < hrp[(size_t)r + 1]; ++k) {
           const int64_t c = hcol[(size_t)k];
           if (c < n_local) P = std::max<int64_t>(P, c > r ? c - r : r - c);
         }
-      std::vector<int> o = chunked_slice_order(in, H, P, oreq == 1 ? 128 : 512);
+      std::vector<int> o = chunked_slice_order(in, H, P, 512);
       if (!o.empty()) {
         in.swap(o);
         A->split_ordered = true;

@@ -100,12 +100,6 @@ constexpr int kVc4Max = 15;  // 4-bit codes: 15 values, 0xf empty
 // template copy of the slice table (CsrDev::sl_t) carries t + 1 in the high
 // half of its width (widths are at most 64).
 constexpr int kVT = 8388608;
-// y-march (variant bit kYM with the march bit 2097152): the
-// plane march's walk along y instead of z on a 3-D 7-point matrix: a wave
-// walks the slices of one half x-line through consecutive y lines (2 KB
-// steps), the +-nx neighbours come from registers and the +-nx*ny ones are
-// the gathers (CsrDev::ymarch_*)
-constexpr int kYM = 16777216;
 // CSR-stream with 16-bit column deltas (bit 128 on the paired loop: 133 =
 // 5 | 128): 10 bytes per entry instead of 12
 constexpr int kC16 = 128;
@@ -180,9 +174,6 @@ struct CsrDev {
   // SELL-P pattern is {-D, (-a,) -1, 0, 1, (a,) D} with D = 128 march_k rows
   // at pool base march_pat; march_len: planes per run (0: fill the grid)
   int march_k = 0, march_a = 0, march_pat = -1, march_len = 0;
-  // the y-march of the same pattern: K = nx / 128 slices per line, the
-  // gathered offset nx * ny (0: no y-march)
-  int ymarch_k = 0, ymarch_a = 0;
   // value-code templates (kVT): the slice table with template ids, the
   // templates (nvt x 64 words of 4-bit codes)
   const SellSlice *sl_t = nullptr;
@@ -207,11 +198,6 @@ struct CsrDev {
 // them, when the requested variant asks for them: spmv_variant keeps kVT and
 // the kernel arguments take the template slice table under exactly this
 // condition.
-// the kernel arguments walk the y-march under exactly this condition
-// (spmv_variant keeps kYM under it too)
-__host__ __device__ inline bool ym_active(const CsrDev &A) {
-  return (A.variant & kYM) && (A.variant & 2097152) && A.ymarch_k > 0 && A.march_pat >= 0;
-}
 __host__ __device__ inline bool vt_active(const CsrDev &A) {
   return (A.variant & kVT) && A.sl_t && A.vct && A.nvt > 0 && A.svc4 && A.svc && A.sl &&
          A.sell_kind && A.sell_maxw <= 8 && (A.variant & 524288) && (A.variant & 262144);
@@ -328,11 +314,8 @@ template <typename T> struct Launch {
 enum { AX_SAPBX = 0, AX_SAMBX = 1, AX_SAXPBY = 2 };
 
 // ---- persistent CG body (mode 5, cgx_coop.hip) -------------------------------
-constexpr int kCoopK = 8;       // entries per row held in registers
-constexpr int kCoopMaxG = 256;     // workgroups: at most one per CU (exchange granules)
-// the register forms' default cap ($CGX_COOP_REG_MAXG); the device's CU
-// count bounds every form (one workgroup per CU)
-constexpr int kCoopMaxGReg = 256;
+constexpr int kCoopK = 8;       // entries per row held in registers (7 in the 1,024-thread form)
+constexpr int kCoopMaxG = 256;  // workgroups: at most one per CU (exchange granules)
 // exchange granules ({tag, half of a double}: two per workgroup and exchange),
 // zeroed before every launch
 struct CoopWs {
@@ -341,25 +324,23 @@ struct CoopWs {
   unsigned int tmo;                      // a workgroup's spin gave up
   unsigned int pad[3];
 };
-// rows per thread (1, 2 or 4; `want` > 0 asks for one) for which n rows fit
-// kCoopMaxGReg workgroups of nt threads (256, or 1024 with one row per
-// thread); 0: none
-int coop_rows_per_thread(int64_t n, int want, int nt, int max_g = kCoopMaxGReg);
-// the streamed form (2): the least R <= kCoopStreamMaxR for which n rows fit
+// the register form: 1 (one row per thread of 1,024) when n rows fit
+// min(max_g, kCoopMaxG) workgroups; 0: none
+int coop_rows_per_thread(int64_t n, int max_g);
+// the streamed form: the least R <= kCoopStreamMaxR for which n rows fit
 // min(max_g, kCoopMaxG) workgroups of 1,024 threads; 0: none
 constexpr int kCoopStreamMaxR = 8;
 int coop_stream_rows(int64_t n, int want, int max_g);
 // up to m bodies from slot0 in one launch (f64, single device): x, r, p0 in
 // and out in the standard layout, p1 scratch (n entries); stops as the
-// three-kernel body does, or sets st->stopped = 4 when a spin gave up
-// form 1 (tagged): p and r handed over as tagged granules in g (6 n words:
-// two p copies, then r); forms 0 and 2: drained write-through stores into r,
-// p0 and p1; form 2 (streamed, NT = 1024) reads the matrix every body
-hipError_t cg_coop(int64_t n, int R, int NT, int form, const int *rowptr, const int *col,
+// three-kernel body does, or sets st->stopped = 4 when a spin gave up.
+// Register form (R = 1) or, `streamed`, the form that reads the matrix every
+// body (R rows per thread of 1,024). hipErrorCooperativeLaunchTooLarge: the
+// occupancy API does not place every workgroup at once.
+hipError_t cg_coop(int64_t n, int R, bool streamed, const int *rowptr, const int *col,
                    const double *val, double *x, double *r, double *p0, double *p1,
-                   unsigned long long *g, CgScalars<double> *st, int slot0, int m, CoopWs *cw,
-                   long long ticks, unsigned long long *trace, int nap, int stall,
-                   hipStream_t s);
+                   CgScalars<double> *st, int slot0, int m, CoopWs *cw, long long ticks,
+                   unsigned long long *trace, int stall, hipStream_t s);
 constexpr int kCoopTraceWords = kCoopMaxG * 8 * 8;  // workgroups x bodies 8-15 x phases
 
 // value-code templates (cgx_abi.cpp build_value_templates): per slice the
@@ -378,6 +359,8 @@ int launch_variant(const CsrDev &A, int dtype);
 // instantiation: a request that resolves to anything else would only fail
 // at its first launch
 bool launch_variant_ok(const CsrDev &A, int dtype);
+// v is a form k_spmv_dot is instantiated for (CGX_SPMV_LIST)
+bool spmv_listed(int v);
 
 // host-side row-block schedule (cgx_abi.cpp)
 std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz,

@@ -156,7 +156,7 @@ __device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T
   return bc;
 }
 
-// Late active check (CGX_LATE_ACTIVE, default on; A/B builds -DCGX_LATE_ACTIVE=0):
+// Late active check (measured in round 2):
 // a body kernel issues its first loads (scalars, partials, first stream
 // block; valid memory whether or not the body runs) together with the
 // active flag and branches on the flag afterwards, so a cache-resident
@@ -164,9 +164,6 @@ __device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T
 // LLVM sinks a load whose only uses lie in one successor of the branch;
 // keep() in the inactive successor uses them there too (an empty asm: it
 // waits for them on that path only), so they stay where they were issued.
-#ifndef CGX_LATE_ACTIVE
-#define CGX_LATE_ACTIVE 1
-#endif
 template <typename T> __device__ __forceinline__ void keep(const T &a) {
   if constexpr (sizeof(T) == 16) {
     asm volatile("" ::"v"(a.x), "v"(a.y));
@@ -184,37 +181,10 @@ template <typename T, int K> __device__ __forceinline__ void keep(const T (&a)[K
 // last arrival of a group sums the group's partials in workgroup order and
 // takes the top ticket; the last group sums the group sums in group order.
 // The result is independent of arrival order. Returns true in that final
-// workgroup, whose thread 0 then holds the totals in v[]. -DCGX_FLAT_TICKET
-// builds the single-ticket form (A/B only).
+// workgroup, whose thread 0 then holds the totals in v[].
 template <typename T, int K>
 __device__ __forceinline__ bool grid_reduce(T (&v)[K], RedWs<T> *ws, T *lds, int *flag) {
   block_sum<T, K>(v, lds);
-#ifdef CGX_FLAT_TICKET
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) store_sc1(&ws->partials[k * kMaxGrid + blockIdx.x], v[k]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&ws->ticket[0], 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (prev == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!*flag) return false;
-  T acc[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    acc[k] = T(0);
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += kBlock)
-      acc[k] += load_sc1(&ws->partials[k * kMaxGrid + i]);
-  }
-  block_sum<T, K>(acc, lds);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = acc[k];
-    __hip_atomic_store(&ws->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return true;
-#else
   const unsigned G = gridDim.x;
   const unsigned g = blockIdx.x % kRedGroups;
   const unsigned ngroups = G < (unsigned)kRedGroups ? G : (unsigned)kRedGroups;
@@ -260,7 +230,6 @@ __device__ __forceinline__ bool grid_reduce(T (&v)[K], RedWs<T> *ws, T *lds, int
     __hip_atomic_store(&ws->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return true;
-#endif
 }
 
 // XCD-grouped logical workgroup id: blocks b and b+8 share an XCD (observed
@@ -362,26 +331,18 @@ __device__ __forceinline__ Int2 tail_cols(Int2 c, int e0, int kk1) {
 // past (Ap after k_update_r, x and the old p buffers in the flushing body):
 // they then leave the cache to the vectors that the next kernel re-reads
 // ("cache policy").
-#ifdef CGX_NO_STREAM_NT
-constexpr bool kStreamNt = false;
-#else
 constexpr bool kStreamNt = true;
-#endif
 // ... but only for vectors too large for the working set to stay in the
 // Infinity Cache: with vectors of <= 32 MB (the 256^3/8 slab's 16.8 MB, the
 // G3 stand-in's 12.7 MB) every vector of the iteration is re-read from it,
 // and plain loads and stores ran the slab bodies 2-3% faster
 // (profiles/r03_slab_nt.log)
-#ifndef CGX_NT_VEC_BYTES
-#define CGX_NT_VEC_BYTES (int64_t(32) << 20)
-#endif
-// loads in flight per thread and trip in k_update_r (A/B: -DCGX_UPDATE_R_UNROLL=8)
-#ifndef CGX_UPDATE_R_UNROLL
-#define CGX_UPDATE_R_UNROLL 4
-#endif
-constexpr int kUR = CGX_UPDATE_R_UNROLL;
+constexpr int64_t kNtVecBytes = int64_t(32) << 20;
+// loads in flight per thread and trip in k_update_r (8 measured slower,
+// DESIGN.md §7)
+constexpr int kUR = 4;
 template <typename T> __device__ __forceinline__ bool stream_nt(int64_t n) {
-  return kStreamNt && n * (int64_t)sizeof(T) > CGX_NT_VEC_BYTES;
+  return kStreamNt && n * (int64_t)sizeof(T) > kNtVecBytes;
 }
 // HIP vector types (double2, float2 of element T): non-temporal through the
 // native vector of two T
@@ -1586,11 +1547,10 @@ __device__ __forceinline__ void spmv_sellpv_march(const CsrArgs &A, const Gather
         T g0[8], g1[8];
         const T left = wave_shr1(ccur.y, b.edge), right = wave_shl1(ccur.x, b.edge);
         constexpr int K1 = S3 ? 2 : 1;  // slot of offset -1
-        // z-march: slots 0 / 6 (-D, +D) from the walk, 1 / 5 (-a, +a)
-        // gathered; y-march (kYM): 1 / 5 (-nx, +nx) from the walk, 0 / 6
-        // (-nx ny, +nx ny) gathered
-        constexpr bool YM = (V & kYM) != 0;
-        constexpr int JM = YM ? 1 : 0, JG = YM ? 0 : 1;
+        // slots 0 / 6 (-D, +D) from the walk, 1 / 5 (-a, +a) gathered (a
+        // y-march, +-nx from the walk and +-nx ny gathered, measured
+        // 93-124 against 72 us at 256^3 in round 3: removed)
+        constexpr int JM = 0, JG = 1;
         g0[JM] = cprev.x;
         g1[JM] = cprev.y;
         if constexpr (S3) {
@@ -1880,11 +1840,7 @@ template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
       PV v;
       v.x = s0;
       v.y = s1;
-#ifdef CGX_AP_NT
-      __builtin_nontemporal_store(v, reinterpret_cast<PV *>(Ap + i));
-#else
       *reinterpret_cast<PV *>(Ap + i) = v;
-#endif
     } else {
       if (l0) Ap[i] = s0;
       if (l1) Ap[i + 1] = s1;
@@ -2077,9 +2033,6 @@ template <int V> struct SpmvWaves {
   // VGPRs, a 12-byte spill) the streamed-code march gets (it took 130 and 3)
   static constexpr int w = (V & 32768) && (V & (65536 | 131072)) ? 8
                            : ((V & kVT) && (V & 2097152)) ? 4
-#ifdef CGX_VT_WAVES  // A/B: the templated consecutive walk held to more waves
-                           : ((V & kVT) && (V & 524288)) ? CGX_VT_WAVES
-#endif
                                                           : 1;
 };
 // k_spmv_fd: the same except the template march (held to 4 waves it
@@ -2201,7 +2154,7 @@ __global__ __launch_bounds__(kBlock, FdWaves<V>::w) void k_spmv_fd(
     int np_rr) {
   __shared__ LdsOf<T, V> sm;
   const int prev = (slot + 3) & 3;
-  // (the flag checked before the partials' loads: CGX_LATE_ACTIVE's form was
+  // (the flag checked before the partials' loads: the late-active form was
   // 0.16 us slower here at 128^2, profiles/r02_late_active.log)
   const long long bodies = st->bodies;
   const bool act = st->active[slot] != 0;
@@ -2394,14 +2347,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // (CG.hpp:396-404, 436: on the r.r the body started with, which k_spmv_fd
   // recorded) and marks the body's x update pending (ran[slot])
   const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
-#if CGX_LATE_ACTIVE
   const bool act = cst->active[slot] != 0;  // branched on after the first loads
-#else
-  if (!st->active[slot]) {
-    if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
-    return;
-  }
-#endif
   __shared__ T red[4];
   __shared__ int flag;
   using V = typename Vec2<T>::V;
@@ -2430,7 +2376,6 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     rv[u] = ri2[j];
     av[u] = ldv<SNT, T>(a2 + j);  // Ap is dead after this kernel
   }
-#if CGX_LATE_ACTIVE
   if (!act) {
     keep(rxr);
     keep(pAp_st);
@@ -2440,7 +2385,6 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
     return;
   }
-#endif
   T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
   if constexpr (PEER) {
     __shared__ double wres;
@@ -2936,10 +2880,6 @@ inline CsrArgs args(const CsrDev &A) {
             A.sl,     A.sdict, A.sidx, A.sval, A.nsl, A.sorder, 0, 0,
             A.smask,  A.nx > 0 ? A.nx : A.n, A.svc, A.svdict, A.svc4,
             A.march_k, A.march_a, A.march_pat, A.march_len};
-  if (ym_active(A)) {  // the y-march walks lines of nx rows, gathers +-nx*ny
-    a.mk = A.ymarch_k;
-    a.mo = A.ymarch_a;
-  }
   if (vt_active(A)) {  // the same condition spmv_variant keeps kVT under
     a.sl = A.sl_t;
     a.vct = static_cast<const unsigned long long *>(A.vct);
@@ -2977,26 +2917,15 @@ __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, 
 }
 
 template <typename T> int Launch<T>::grid_rows(int nrb) {
-  static const int cap = [] {  // $CGX_SPMV_GRID: A/B only
-    const char *e = std::getenv("CGX_SPMV_GRID");
-    const int v = e ? std::atoi(e) : 0;
-    return (v >= 64 && v <= kMaxGrid) ? v : kMaxGrid;
-  }();
-  return nrb < cap ? (nrb < 1 ? 1 : nrb) : cap;
+  return nrb < kMaxGrid ? (nrb < 1 ? 1 : nrb) : kMaxGrid;
 }
 // Streaming kernels: at most `cap` workgroups, each walking its share in a
 // grid-stride loop. Fewer, longer-lived workgroups stream better than the
 // 8-per-CU persistent grid the SpMV uses: k_update_r 256 (1 per CU), the
 // x/p updates 512 (2 per CU; the flushing body keeps 8 streams in flight);
 // A/B in DESIGN.md §4 (gpurun_out r44/r45).
-#ifndef CGX_GRID_UPDATE_R
-#define CGX_GRID_UPDATE_R 256
-#endif
-#ifndef CGX_GRID_UPDATE_P
-#define CGX_GRID_UPDATE_P 512
-#endif
-constexpr int kGridUpdateR = CGX_GRID_UPDATE_R;  // A/B builds: EXTRA=-DCGX_GRID_UPDATE_R=...
-constexpr int kGridUpdateP = CGX_GRID_UPDATE_P;
+constexpr int kGridUpdateR = 256;
+constexpr int kGridUpdateP = 512;
 template <typename T> int Launch<T>::grid_elems(int64_t n, int cap) {
   int64_t g = (n + (int64_t)kBlock * 8 - 1) / ((int64_t)kBlock * 8);
   if (g < 1) g = 1;
@@ -3021,7 +2950,6 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
                                                     CgScalars<T> *st, int slot, RedWs<T> *ws,
                                                     int np_rr, int rev, const PeerDev *PD) {
   const int nxt = (slot + 1) & 3;
-#if CGX_LATE_ACTIVE
   // the flag, rxr and the r.r partials in one round trip
   const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
   const bool act = cst->active[slot] != 0;
@@ -3038,15 +2966,6 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   }
   __shared__ T red[4];
   T rr = np_rr > 0 ? parts_sum(pl, np_rr, red) : rr_st;
-#else
-  if (!st->active[slot]) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
-    return;
-  }
-  __shared__ T red[4];
-  const T rxr = st->rxr[slot];
-  T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
-#endif
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
@@ -3316,7 +3235,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
              (v & (16 | 2 | 65536 | 131072 | (A.svc4 ? 262144 : 0) |
                    (A.sell_maxw <= 8 ? 524288 | 1048576 : 0) |
                    (A.sell_maxw <= 8 && A.march_k > 0 ? 2097152 : 0))) |
-             (vt_active(A) ? kVT : 0) | (ym_active(A) && A.sell_maxw <= 8 ? kYM : 0);
+             (vt_active(A) ? kVT : 0);
     if (A.sl && A.sell_kind) return 8192 | (A.sell_kind == 2 ? 16384 : 0) | (v & (16 | 2));
     if (A.sl && A.sell_r == 2) return 2048 | 4096 | (v & (16 | 2));
     if (A.sl) return v & (2048 | 16 | 2 | (A.sell_maxw <= 8 ? 8 : 0));
@@ -3419,8 +3338,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 // x CUs; 0: unknown variant). The SpMV grid is capped to it: a persistent
 // grid larger than what fits runs its last workgroups as a second wave,
 // after the first ones finish their fixed shares, and that tail measured
-// 8% of the value-code kernel at 256^3 (tools/gpu_vc_ab.sh). $CGX_SPMV_RESIDENT=0
-// turns the cap off (A/B).
+// 8% of the value-code kernel at 256^3 (tools/gpu_vc_ab.sh).
 #define CGX_SPMV_LIST(X)                                                                    \
   X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(264) X(265) X(266)      \
   X(133) X(135)                                                                             \
@@ -3440,11 +3358,6 @@ template <typename T> const void *spmv_dot_kernel(int v) {
 }
 
 template <typename T> int spmv_dot_resident(int v) {
-  static const bool on = [] {
-    const char *e = std::getenv("CGX_SPMV_RESIDENT");
-    return !e || std::atoi(e) != 0;
-  }();
-  if (!on) return 0;
   static std::mutex mu;
   static std::map<std::pair<int, int>, int> cache;  // (device, variant) -> workgroups
   int dev = 0;
@@ -3907,6 +3820,8 @@ int launch_variant(const CsrDev &A, int dtype) {
   return (dtype == 1 /* CGX_F32 */ ? spmv_variant<float>(A) : spmv_variant<double>(A)) |
          (vl_active(A) ? kVL : 0);
 }
+
+bool spmv_listed(int v) { return spmv_dot_kernel<double>(v) != nullptr; }
 
 bool launch_variant_ok(const CsrDev &A, int dtype) {
   return dtype == 1 /* CGX_F32 */ ? spmv_dot_kernel<float>(spmv_variant<float>(A)) != nullptr

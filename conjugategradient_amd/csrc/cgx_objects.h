@@ -191,13 +191,9 @@ struct cgx_cg {
   bool fdefer = false;  // mode 4: p update folded into the SpMV, x deferred as mode 3
   bool coop = false;    // mode 5: persistent body, one launch per chunk (cgx_coop.hip)
   int coop_r = 0;       // its rows per thread
-  int coop_nt = 1024;   // threads per workgroup ($CGX_COOP_NT: 256, 512 or 1024)
-  int coop_nap = 1;     // s_sleep(1)s per exchange poll ($CGX_COOP_NAP)
   int coop_stall = -1;  // tests: a launch's body whose p.Ap partial workgroup 0
                         // withholds ($CGX_COOP_INJECT_STALL; -1 none)
   void *coop_ws = nullptr;  // cgx::CoopWs
-  void *coop_rg = nullptr;  // tagged p and r granules (6 n words; $CGX_COOP_TAGR=1)
-  bool coop_tagr = false;
   bool coop_stream = false;  // form 2: the matrix read every body (k_cg_coop_st)
   int coop_stream_want = -1; // $CGX_COOP_STREAM: -1 auto, 0 never, 1 always
   void *coop_trace = nullptr;  // $CGX_COOP_TRACE: phase stamps (cgx_cg_coop_trace)

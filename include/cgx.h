@@ -213,13 +213,13 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
  * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
-/* mode 5's launch shape: rows per thread, threads per workgroup ($CGX_COOP_NT,
- * default 1024), workgroups, and the form: 0 register form with drained
- * write-through stores (default), 1 register form with p and r handed over
- * as tagged granules ($CGX_COOP_TAGR=1), 2 the streamed form (the matrix
- * read every body, entries staged through LDS) */
+/* mode 5's launch shape: rows per thread, threads per workgroup (1024),
+ * workgroups, and the form: 0 the register form (drained write-through
+ * stores), 2 the streamed form (the matrix read every body, entries staged
+ * through LDS; $CGX_COOP_STREAM=1 forces it, $CGX_COOP_R its rows per
+ * thread) */
 int cgx_cg_coop_shape(cgx_cg *cg, int *rows_per_thread, int *threads, int *workgroups,
-                      int *tagged);
+                      int *form);
 /* diagnostics: with $CGX_COOP_TRACE=1 set before mode 5 is chosen, the
  * wall-clock stamps (100 MHz) of the last launch: [workgroup][body 8..15]
  * [phase 0..7] (0 body start, 1 SpMV done, 2 p.Ap partial ready, 3 p.Ap

@@ -38,18 +38,10 @@ def _solve(queue, m, b, mode, tol, max_iter=-1, x0=None, poll=32, shape=None):
     return cg.extract(), cg.iterations, cg.final_rxr
 
 
-SHAPES = [("1", "256", "0"), ("2", "256", "0"), ("4", "256", "0"), ("1", "512", "0"),
-          ("1", "1024", "0"), ("1", "256", "1"), ("2", "256", "1"), ("1", "512", "1")]
-
-
-@pytest.mark.parametrize("R,NT,tagged", SHAPES, ids=["-".join(s) for s in SHAPES])
 @pytest.mark.parametrize("dims", [(2, 128, 128, 1), (3, 20, 18, 17), (2, 70, 66, 1)],
                          ids=["p2d_128", "p3d_20x18x17", "p2d_70x66"])
-def test_mode5_fixed_bodies_match_oracle(queue, oracle, monkeypatch, dims, R, NT, tagged):
-    """rows per thread x threads per workgroup x hand-off form"""
-    monkeypatch.setenv("CGX_COOP_R", R)
-    monkeypatch.setenv("CGX_COOP_NT", NT)
-    monkeypatch.setenv("CGX_COOP_TAGR", tagged)
+def test_mode5_fixed_bodies_match_oracle(queue, oracle, dims):
+    """the register form (one row per thread of 1,024)"""
     rp, cl, vl = oracle.poisson(*dims)
     n = len(rp) - 1
     m = cga.Matrix(queue, vl, cl, rp)
@@ -237,27 +229,6 @@ def test_mode5_refused_where_it_does_not_apply(queue, oracle):
             assert _shape(h)[3] == form
         finally:
             L.cgx_cg_destroy(h)
-
-
-@pytest.mark.parametrize("tagr", ["0", "1"])
-def test_mode5_r_handoff_forms(queue, oracle, monkeypatch, tagr):
-    """p and r handed over as drained write-through stores (default) or as
-    tagged granules with the next body's gathers overlapping the r.r exchange
-    ($CGX_COOP_TAGR=1): the same values bit for bit (only the hand-off
-    differs), matching the oracle."""
-    monkeypatch.setenv("CGX_COOP_TAGR", tagr)
-    rp, cl, vl = oracle.poisson(2, 128, 128, 1)
-    n = len(rp) - 1
-    m = cga.Matrix(queue, vl, cl, rp)
-    b = np.arange(1, n + 1, dtype=np.float64)
-    x5, it5, r5 = _solve(queue, m, b, 5, 0.0, max_iter=60, poll=4)
-    monkeypatch.setenv("CGX_COOP_TAGR", "1" if tagr == "0" else "0")
-    x5b, it5b, r5b = _solve(queue, m, b, 5, 0.0, max_iter=60, poll=4)
-    assert it5 == it5b == 60
-    np.testing.assert_array_equal(x5, x5b)
-    assert r5 == r5b
-    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 60, 8)
-    assert rel(x5, xr) <= 1e-10
 
 
 @pytest.mark.parametrize("stream", ["0", "1"])

@@ -84,17 +84,6 @@ def test_async_host_halo_matches_synchronous(nproc, grid, mode):
     assert ra["x_sha"] == rs["x_sha"]
 
 
-@pytest.mark.parametrize("nproc,mode", [(3, 3), (2, 1)])
-def test_peer_boundary_without_the_folded_wait(nproc, mode):
-    """The boundary slices wait for the pushes themselves and read the ghosts
-    from the landing buffer (k_spmv_dot_bnd, the default above); with
-    $CGX_PEER_WAIT_FOLD=0 the separate k_peer_wait copies them into p's
-    ghost tail first. Both match the oracle."""
-    r = _run(nproc, "host-peer", 20, mode, env={"CGX_PEER_WAIT_FOLD": "0"})
-    assert r["ok"], r
-    assert r["peer"] == [1] * nproc
-
-
 def test_partitioned_slab_of_the_8gpu_config():
     """BASELINE config 4's per-rank shape: 512^3 over 8 GPUs gives each rank a
     512 x 512 x 64 slab and 2 MiB halo planes. Two such slabs (global

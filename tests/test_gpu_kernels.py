@@ -277,15 +277,13 @@ def test_fused_split_runs(queue, oracle, mode):
     assert rel(xs[(23,)], xr) <= 1e-12
 
 
-@pytest.mark.parametrize("staged", ["1", "0"])
-def test_large_host_copies_round_trip(queue, monkeypatch, staged):
+def test_large_host_copies_round_trip(queue):
     """cgx_h2d / cgx_d2h: device->host copies >= 16 MiB go through the pinned
-    ring (64 MiB chunks, $CGX_STAGED=0 turns it off); sizes that are not a
-    chunk multiple, unaligned pointers."""
+    ring (64 MiB chunks); sizes that are not a chunk multiple, unaligned
+    pointers."""
     import ctypes as C
 
     from conjugategradient_amd._native import check, lib
-    monkeypatch.setenv("CGX_STAGED", staged)
     L = lib()
     nbytes = 150 * (1 << 20) + 13
     src = np.random.default_rng(5).integers(0, 256, nbytes, dtype=np.uint8)

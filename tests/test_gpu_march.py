@@ -6,8 +6,8 @@ pair in registers (cgx_kernels.hip spmv_sellpv_march). Its row sums run in
 the same slot order as every SELL-P form, so the bar is bit-exactness with
 the oracle's restatement of the reference SpMV (VectorOperations.hpp:438-466)
 on every geometry the plan accepts (3-D 7-point and 2-D 5-point with the
-plane a multiple of 128 rows, ragged last planes, runs of 1..n planes) and a
-silent fallback to the per-slice form where it does not apply.
+plane a multiple of 128 rows, ragged last planes) and a silent fallback to
+the per-slice form where it does not apply.
 """
 import ctypes as C
 
@@ -49,16 +49,13 @@ GEOMS = [
 
 
 @pytest.mark.parametrize("geom", GEOMS, ids=lambda g: "x".join(map(str, g[:4])))
-@pytest.mark.parametrize("run", [0, 1, 3])
-def test_march_spmv_bitexact(queue, oracle, monkeypatch, geom, run):
+def test_march_spmv_bitexact(queue, oracle, geom):
     dim, nx, ny, nz, K, a = geom
-    if run:
-        monkeypatch.setenv("CGX_MARCH_LEN", str(run))
     rp, cl, vl = oracle.poisson(dim, nx, ny, nz)
     n = len(rp) - 1
     A = Matrix(queue, vl, cl, rp)
     check(lib().cgx_csr_set_sell(A.schedule(), 3))
-    assert march_info(A) == (K, a, run)
+    assert march_info(A) == (K, a, 0)  # run length 0: fill the grid's waves
     x = np.random.default_rng(11).standard_normal(n)
     out = spmv_all(queue, A, x, MARCH + STENCIL + [PLAIN])
     ref = oracle.spmv(rp, cl, vl, x)
@@ -89,14 +86,6 @@ def test_march_not_planned(queue, oracle, dims):
     x = np.random.default_rng(4).standard_normal(len(rp) - 1)
     out = spmv_all(queue, A, x, MARCH[-1:])
     np.testing.assert_array_equal(out[MARCH[-1]], oracle.spmv(rp, cl, vl, x))
-
-
-def test_march_off_by_env(queue, oracle, monkeypatch):
-    monkeypatch.setenv("CGX_MARCH", "0")
-    rp, cl, vl = oracle.poisson(3, 32, 32, 8)
-    A = Matrix(queue, vl, cl, rp)
-    check(lib().cgx_csr_set_sell(A.schedule(), 3))
-    assert march_info(A) == (0, 0, 0)
 
 
 def test_march_nonfinite_x(queue, oracle):

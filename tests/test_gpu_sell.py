@@ -72,9 +72,7 @@ def _sell_info(m):
 @pytest.mark.parametrize("case", ["poisson2d", "poisson3d_ragged", "poisson3d_wide", "banded",
                                   "empty_rows", "tiny"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype, R, monkeypatch):
-    if case == "poisson3d_wide":
-        monkeypatch.setenv("CGX_SELL_ORDER", "1")   # the opt-in visit order
+def test_sell_spmv_bitexact_all_variants(queue, oracle, case, dtype, R):
     rp, cl, vl = _matrix_cases(oracle)[case]
     n = len(rp) - 1
     A = Matrix(queue, vl, cl, rp, dtype=dtype)
@@ -125,11 +123,15 @@ def test_sell_not_built_for_scattered_matrix(queue):
         check(lib().cgx_csr_set_variant(A.schedule(), 9999))
 
 
-def test_sell_disabled_by_env(queue, oracle, monkeypatch):
-    monkeypatch.setenv("CGX_SELL", "0")
+def test_sell_dropped_on_request(queue, oracle):
     rp, cl, vl = oracle.poisson(2, 32, 32, 1)
     A = Matrix(queue, vl, cl, rp)
+    assert _sell_info(A)[0] == 3
+    check(lib().cgx_csr_set_sell(A.schedule(), 0))
     assert _sell_info(A)[0] == 0
+    v = C.c_int()
+    check(lib().cgx_csr_variant(A.schedule(), C.byref(v)))
+    assert not v.value & (2048 | 8192)
 
 
 @pytest.mark.parametrize("R", [1, 2, 3])
@@ -158,14 +160,13 @@ def test_sell_spmv_nonfinite_and_signed_zero(queue, oracle, R):
 
 @pytest.mark.parametrize("sell", ["1", "2", "3", "0"])
 @pytest.mark.parametrize("dim,n", [(2, 64), (3, 20), (3, 0)])
-def test_cg_both_formats_match_oracle(oracle, monkeypatch, sell, dim, n):
-    monkeypatch.setenv("CGX_SELL", sell)
-    monkeypatch.setenv("CGX_SELL_ORDER", "1")
-    # n = 0: 256 x 130 x 3, wide planes (the visit-order path)
+def test_cg_both_formats_match_oracle(oracle, sell, dim, n):
+    # n = 0: 256 x 130 x 3, wide planes
     rp, cl, vl = oracle.poisson(dim, n, n, n) if n else oracle.poisson(3, 256, 130, 3)
     b = np.arange(1, len(rp), dtype=np.float64)
     cg = cga.CG.createCG()
     cg.setMatrix(vl, cl, rp)
+    check(lib().cgx_csr_set_sell(cg.A.schedule(), int(sell)))
     cg.setTarget(b)
     cg.solve(1e-8)
     v = C.c_int()
@@ -183,8 +184,6 @@ def test_auto_visit_order_on_large_planes(queue, oracle, monkeypatch):
     stays bit-exact against the oracle in the production form and in
     CSR-stream, and CG holds the oracle's iterates (only the p.Ap partials'
     grouping changes)."""
-    monkeypatch.delenv("CGX_SELL_ORDER", raising=False)
-    monkeypatch.delenv("CGX_SELL_ORDER_CHUNK", raising=False)
     rp, cl, vl = oracle.poisson(3, 512, 256, 4)  # planes of 131,072 rows = 1,024 slices
     n = len(rp) - 1
     A = Matrix(queue, vl, cl, rp)

@@ -5,7 +5,7 @@ the same iteration as bench.py (auto mode, graph replay), no halo and no
 all-reduce. Its time per body is the floor of an 8-GPU body: the work each
 GPU does plus the launch boundaries, without the transport.
 
-    python tools/slab_bench.py [dim,nx,ny,nz,bodies ...]
+    python tools/slab_bench.py [--mode M] [dim,nx,ny,nz,bodies ...]   (M 0: auto)
 """
 from __future__ import annotations
 
@@ -28,8 +28,13 @@ def main():
     L = lib()
     q = cga.Queue(0)
     shapes = ((3, 256, 256, 32, 2000), (3, 512, 512, 64, 400))
-    if len(sys.argv) > 1:  # e.g. 2,4096,4096,1,400
-        shapes = tuple(tuple(int(v) for v in a.split(",")) for a in sys.argv[1:])
+    args = sys.argv[1:]
+    want_mode = 0
+    if len(args) >= 2 and args[0] == "--mode":
+        want_mode = int(args[1])
+        args = args[2:]
+    if args:  # e.g. 2,4096,4096,1,400
+        shapes = tuple(tuple(int(v) for v in a.split(",")) for a in args)
     for dim, nx, ny, nz, steps in shapes:
         A = cga.Matrix.poisson(q, dim, nx, ny, nz)
         n = A.N()
@@ -41,6 +46,7 @@ def main():
         cg = C.c_void_p()
         check(L.cgx_cg_create(q.handle, sched, C.byref(cg)))
         check(L.cgx_cg_config(cg, 64, 1))
+        check(L.cgx_cg_set_mode(cg, want_mode))
         mode, v = C.c_int(), C.c_int()
         check(L.cgx_cg_get_mode(cg, C.byref(mode)))
         check(L.cgx_csr_variant(sched, C.byref(v)))
