@@ -247,6 +247,62 @@ def cpu_baseline(workload: str, grid, threads: int, budget_s: float):
     }
 
 
+def rccl_timing(L, q, args, wl, b, x, transport, its, elapsed, world, dist) -> dict:
+    """The same bodies over RCCL (ncclSend/Recv halo on the comm stream
+    beside the interior slices, ncclAllReduce for p.Ap and r.r; SURVEY
+    §8(e), the north star's transport) when the timed run used the device
+    peer transport: a second partitioned matrix without the peer transport,
+    the same warmup and steps, max over ranks. `skipped` says why not."""
+    import torch
+
+    from conjugategradient_amd._native import F64, check
+
+    if transport == "rccl":
+        return {"iterations_per_s": round(its, 2), "ms_per_step": round(elapsed / args.steps * 1e3,
+                                                                         4),
+                "note": "the timed run itself (RCCL carried it)"}
+    if not transport.startswith("peer (setup: rccl"):
+        return {"skipped": f"no RCCL communicator (setup transport {transport!r}: RCCL refuses "
+                           "ranks that share one GPU, so the one-GPU rehearsal runs the host "
+                           "transport)"}
+    A2 = C.c_void_p()
+    check(L.cgx_csr_create_dist(q.handle, wl.n_global, wl.row_begin, wl.n_local, wl.nnz_local,
+                                wl.rows.ptr, wl.cols.ptr, wl.vals.ptr, F64, C.byref(A2)))
+    cg = C.c_void_p()
+    check(L.cgx_cg_create(q.handle, A2, C.byref(cg)))
+    check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
+    check(L.cgx_cg_set_mode(cg, args.mode))
+    x.fill(0.0)
+    check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, args.warmup + args.steps))
+    bodies, stopped = C.c_int64(0), C.c_int(0)
+    if args.warmup:
+        check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
+    check(L.cgx_cg_prepare(cg, args.steps))
+    q.wait()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    check(L.cgx_cg_run(cg, args.steps, C.byref(bodies), C.byref(stopped)))
+    q.wait()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = t1 - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ok = bodies.value - args.warmup == args.steps
+    check(L.cgx_cg_destroy(cg))
+    check(L.cgx_csr_destroy(A2))
+    if not ok:
+        return {"skipped": f"the RCCL run stopped early (stopped={stopped.value})"}
+    return {"iterations_per_s": round(args.steps / el, 2),
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "note": "the same workload and bodies over RCCL (halo: ncclSend/Recv on the comm "
+                    "stream; dots: ncclAllReduce), no device peer transport"}
+
+
 # ---------------------------------------------------------------------------
 # the measured run (one rank)
 # ---------------------------------------------------------------------------
@@ -271,12 +327,15 @@ def run(args) -> None:
     # ---- communicator (N > 1) ----------------------------------------------
     transport = "single"
     rccl_note = None
+    # the distributed path: N > 1, or --transport rccl at N = 1 (the RCCL
+    # iteration on one rank: all-reduces over a one-rank communicator)
+    dist_on = world > 1 or args.transport == "rccl"
     if world > 1 and args.transport in ("host", "host-peer"):
         from conjugategradient_amd.hostcomm import HostTransport
         ht = HostTransport()
         ht.attach(q)
         transport = "host"
-    elif world > 1:
+    elif dist_on:
         # RCCL; with --transport auto, a node where it does not come up
         # (every rank's outcome, agreed over gloo) keeps the host transport
         # for setup and tries the device peer transport for the iteration
@@ -285,14 +344,16 @@ def run(args) -> None:
         if rank == 0:
             rc = L.cgx_nccl_unique_id(uid, 128)
         obj = [(bytes(uid.raw), rc) if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0)
         if obj[0][1] == 0:
             rc = L.cgx_dist_init(q.handle, rank, world, obj[0][0], 128)
         else:
             rc = obj[0][1]
         why = L.cgx_last_error().decode() if rc else ""
         ok = torch.tensor([0.0 if rc == 0 else 1.0], dtype=torch.float64)
-        dist.all_reduce(ok)
+        if world > 1:
+            dist.all_reduce(ok)
         if ok.item() == 0.0:
             transport = "rccl"
         elif args.transport == "auto":
@@ -321,7 +382,7 @@ def run(args) -> None:
     check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(row_begin)))
     x.fill(0.0)
     A = C.c_void_p()
-    if world > 1:
+    if dist_on:
         check(L.cgx_csr_create_dist(q.handle, n_global, row_begin, n_local, nnz_local,
                                     wl.rows.ptr, wl.cols.ptr, wl.vals.ptr, F64, C.byref(A)))
     else:
@@ -405,6 +466,11 @@ def run(args) -> None:
     if ran != args.steps:
         raise RuntimeError(f"ran {ran} iterations, expected {args.steps} (stopped={stopped.value})")
     its = args.steps / elapsed
+    # the north star's transport (RCCL halo + all-reduces) timed beside the
+    # device peer one when the peer transport carried the run
+    rccl_iteration = None
+    if dist_on:
+        rccl_iteration = rccl_timing(L, q, args, wl, b, x, transport, its, elapsed, world, dist)
 
     # compulsory bytes of one iteration in the streamed formats, all ranks
     spmv_fmt_local = spmv_bytes_per_iter(sbytes.value, n_local, mode_eff)
@@ -514,6 +580,7 @@ def run(args) -> None:
                        "transport": transport,
                        "peer_fallback_reason": peer_note,
                        "rccl_note": rccl_note,
+                       "rccl_iteration": rccl_iteration,
                        "transport_validation": validation,
                        "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies",

@@ -113,6 +113,24 @@ def test_bench_two_ranks_validates_peer_transport():
     assert v["ok"], v
     assert v["x_rel_peer_vs_setup"] <= 1e-10
     assert line["config"]["transport"].startswith("peer")
+    # the RCCL iteration beside it: not on one GPU (RCCL refuses shared devices)
+    assert "RCCL" in line["config"]["rccl_iteration"]["skipped"]
+
+
+def test_bench_rccl_iteration_at_world_size_one():
+    """--transport rccl at N = 1: the partitioned path over a one-rank RCCL
+    communicator (the all-reduces run, no halo), timed as the line's value
+    and reported as its rccl_iteration."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--grid", "64",
+           "--steps", "20", "--warmup", "5", "--transport", "rccl", "--no-cpu", "--no-general",
+           "--profile-steps", "0"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = line["config"]
+    assert cfg["transport"] == "rccl"
+    r = cfg["rccl_iteration"]
+    assert r["iterations_per_s"] == line["iterations_per_s"] and r["ms_per_step"] > 0
 
 
 def test_bench_two_ranks_auto_transport_on_one_gpu():
