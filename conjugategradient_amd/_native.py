@@ -60,6 +60,8 @@ _SIGS = {
     "cgx_csr_create": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _i32, _vp, C.POINTER(_vp)]),
     "cgx_csr_destroy": (_i32, [_vp]),
     "cgx_csr_set_tile": (_i32, [_vp, _i32]),
+    "cgx_csr_set_block_order": (_i32, [_vp, _i32]),
+    "cgx_csr_block_order_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     "cgx_csr_variant": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_set_variant": (_i32, [_vp, _i32]),
     "cgx_csr_set_sell": (_i32, [_vp, _i32]),
@@ -143,6 +145,8 @@ def lib() -> C.CDLL:
                            "make -C conjugategradient_amd/csrc")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("CGX_LIB") and not hasattr(L, name):
+                continue  # an older A/B build ($CGX_LIB) without this entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

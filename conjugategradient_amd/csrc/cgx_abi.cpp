@@ -811,6 +811,124 @@ static bool build_col16(cgx_csr *A) {
   return true;
 }
 
+// CSR-stream's row-block visit order (CsrDev::rbo). A matrix from a 3-D
+// grid gathers p at +-D (one plane) from every row; in the natural order the
+// XCD's workgroups reach a plane's rows again only after ~2 D rows of val/col
+// have streamed through its 4 MB L2, so the p lines at +-D are fetched again
+// (round 3's PMC: 1.19x the CSR bytes at 256^3). Walking chunks of W rows of
+// a plane through all planes of the XCD's eighth puts them W rows apart.
+static void free_block_order(cgx_csr *A) {
+  if (A->d_rbo) (void)hipFree(A->d_rbo);
+  A->d_rbo = nullptr;
+  A->dev.rbo = nullptr;
+  A->dev.ob_D = A->dev.ob_W = 0;
+}
+
+// The largest positive column offset (col - row) that at least a quarter of
+// a sample of rows has (64 runs of 64 rows, evenly spaced); 0 when none.
+static int dominant_offset(cgx_csr *A, const int *hrp) {
+  const int64_t n = A->dev.n;
+  if (n < 4096 || A->dev.nnz < 1) return 0;
+  hipStream_t s = A->ctx->stream;
+  std::unordered_map<int, int> cnt;
+  int rows = 0;
+  std::vector<int> c;
+  for (int i = 0; i < 64; ++i) {
+    const int64_t r0 = (int64_t)i * (n - 64) / 63;
+    const int k0 = hrp[r0], k1 = hrp[r0 + 64];
+    if (k1 <= k0) continue;
+    c.resize((size_t)(k1 - k0));
+    if (hipMemcpyAsync(c.data(), A->dev.col + k0, c.size() * sizeof(int), hipMemcpyDeviceToHost,
+                       s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    for (int64_t r = r0; r < r0 + 64; ++r) {
+      ++rows;
+      for (int k = hrp[r]; k < hrp[r + 1]; ++k) {
+        const int64_t o = (int64_t)c[(size_t)(k - k0)] - r;
+        if (o > 0 && o < (int64_t(1) << 30)) ++cnt[(int)o];
+      }
+    }
+  }
+  int D = 0;
+  for (const auto &kv : cnt)
+    if (4 * kv.second >= rows && kv.first > D) D = kv.first;
+  return D;
+}
+
+// Build the order: W > 0 chunk rows, W < 0 automatic. Returns CGX_OK with no
+// order when the matrix has no plane offset worth it (automatic) or refuses
+// an explicit W then.
+static int build_block_order(cgx_csr *A, int W) {
+  free_block_order(A);
+  if (W == 0) return CGX_OK;
+  const int64_t n = A->dev.n;
+  const int nrb = A->dev.nrb;
+  DeviceGuard g(A->ctx->device);
+  hipStream_t s = A->ctx->stream;
+  std::vector<int> hrp((size_t)n + 1), rb((size_t)nrb + 1);
+  CGX_HIP(hipMemcpyAsync(hrp.data(), A->dev.rowptr, hrp.size() * sizeof(int),
+                         hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipMemcpyAsync(rb.data(), A->dev.rb, rb.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+  CGX_HIP(hipStreamSynchronize(s));
+  const int D = dominant_offset(A, hrp.data());
+  // planes of the XCD's eighth, and the rows its 256 workgroups hold at once
+  const int64_t Z = D > 0 ? (n / 8) / D : 0;
+  const double bpr = 12.0 * (double)A->dev.nnz / (double)n + 16.0;
+  const int64_t R = 256 * ((n + nrb - 1) / nrb);
+  if (W < 0) {
+    // worth it when two planes of stream overflow half an L2 and the eighth
+    // holds several planes
+    if (D <= 0 || Z < 4 || 2.0 * D * bpr < 2.0 * (1 << 20)) return CGX_OK;
+    W = (int)std::max<int64_t>(R / Z, (n + nrb - 1) / nrb);
+  } else if (D <= 0 || Z < 2) {
+    set_error("block order: the matrix has no dominant plane offset (D = %d, %lld planes per "
+              "XCD eighth)", D, (long long)Z);
+    return CGX_EINVAL;
+  }
+  std::vector<int> ord((size_t)nrb);
+  for (int gi = 0; gi < 8; ++gi) {
+    const int lo = (int)(((int64_t)nrb * gi) >> 3), hi = (int)(((int64_t)nrb * (gi + 1)) >> 3);
+    if (hi <= lo) continue;
+    const int64_t base = rb[(size_t)lo];
+    for (int b = lo; b < hi; ++b) ord[(size_t)b] = b;
+    std::stable_sort(ord.begin() + lo, ord.begin() + hi, [&](int x, int y) {
+      const int64_t ux = rb[(size_t)x] - base, uy = rb[(size_t)y] - base;
+      const int64_t cx = (ux % D) / W, cy = (uy % D) / W;
+      if (cx != cy) return cx < cy;
+      return ux / D < uy / D;
+    });
+  }
+  void *d = nullptr;
+  CGX_HIP(hipMalloc(&d, ord.size() * sizeof(int)));
+  hipError_t e = hipMemcpyAsync(d, ord.data(), ord.size() * sizeof(int), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return hip_fail(e, "build_block_order");
+  }
+  A->d_rbo = d;
+  A->dev.rbo = (const int *)d;
+  A->dev.ob_D = D;
+  A->dev.ob_W = W;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_set_block_order(cgx_csr *A, int chunk_rows) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  CGX_REQUIRE(chunk_rows >= -1, CGX_EINVAL, "chunk_rows must be >= -1");
+  return build_block_order(A, chunk_rows);
+}
+
+extern "C" int cgx_csr_block_order_info(cgx_csr *A, int *D, int *chunk_rows) {
+  CGX_REQUIRE(A && D && chunk_rows, CGX_EINVAL, "NULL argument");
+  *D = A->dev.rbo ? A->dev.ob_D : 0;
+  *chunk_rows = A->dev.rbo ? A->dev.ob_W : 0;
+  return CGX_OK;
+}
+
 // ===========================================================================
 // CSR
 // ===========================================================================
@@ -892,6 +1010,7 @@ static void csr_free(cgx_csr *A) {
     if (A->d_ext) (void)hipFree(A->d_ext);
     free_sell(A);
     free_col16(A);
+    free_block_order(A);
     peer_destroy(A);
     dist_destroy_halo(A);
   }
@@ -921,6 +1040,7 @@ extern "C" int cgx_csr_set_tile(cgx_csr *A, int tile) {
   CGX_HIP(hipMalloc(&d, rb.size() * sizeof(int)));
   CGX_HIP(hipMemcpyAsync(d, rb.data(), rb.size() * sizeof(int), hipMemcpyHostToDevice, s));
   CGX_HIP(hipStreamSynchronize(s));
+  free_block_order(A);  // an order of the old blocks
   if (A->d_rb) CGX_HIP(hipFree(A->d_rb));
   A->d_rb = d;
   A->dev.rb = d;
@@ -953,7 +1073,7 @@ void free_lean(cgx_csr *A) {
   A->dev.vl_cls = nullptr;
   A->dev.vl_tab = nullptr;
   A->dev.vl_grid = A->dev.vl_nst = A->dev.vl_D = A->dev.vl_a = 0;
-  A->dev.vl_P = A->dev.vl_K = 0;
+  A->dev.vl_P = A->dev.vl_K = A->dev.vl_lds = 0;
   A->dev.lean = false;
   A->vl_slice_cls.clear();
   A->vl_ncls = 0;
@@ -1649,6 +1769,11 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
   A->dev.vl_nst = (int)nst;
   A->dev.vl_P = (int)P;
   A->dev.vl_K = chunked ? (int)K : 0;
+  // the per-slice form's slices: a few (256^3: 8) read the dictionary where
+  // it lies; many (512^3: 1,036) are cheaper from an LDS copy
+  int64_t generic = 0;
+  for (unsigned char c : A->vl_slice_cls) generic += c == 0xff;
+  A->dev.vl_lds = generic >= 64 ? 1 : 0;
   A->vl_ncls = (int)tab.size();
   return CGX_OK;
 }
@@ -1696,7 +1821,7 @@ int build_value_codes(cgx_csr *A) {
 // SELL copy of A on the device with R rows per lane (0: the default layout),
 // when the matrix qualifies (sell_plan_host); otherwise A keeps only the
 // CSR-stream schedule and this returns CGX_OK. Errors are device failures
-// only. $CGX_SELL=0 disables it, =1 / =2 selects R.
+// only. cgx_csr_set_sell selects R (0 drops the copy).
 int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   // R: 1 / 2 dictionary SELL with R rows per lane, 3 SELL-P (2 rows per
   // lane), 0 the default: SELL-P where the matrix qualifies, else R = 2

@@ -190,7 +190,13 @@ struct CsrDev {
   const VlClass *vl_tab = nullptr;
   int vl_grid = 0, vl_nst = 0, vl_D = 0, vl_a = 0;
   int vl_P = 0, vl_K = 0;  // the chunked walk's planes per XCD group, slices per plane
+  int vl_lds = 0;  // the per-slice form's dictionary and templates copied to LDS first
   bool lean = false;
+  // CSR-stream block visit order (cgx_abi.cpp build_block_order; null:
+  // natural): walk position -> row block, a permutation within each XCD
+  // eighth that walks chunks of ob_W rows through planes ob_D rows apart
+  const int *rbo = nullptr;
+  int ob_D = 0, ob_W = 0;
 };
 
 // The templates apply to the pipelined 4-bit value-code walks (bits 524288,

@@ -282,7 +282,19 @@ struct CsrArgs {
   const VlClass *vl_tab;
   int vl_nst, vl_D, vl_a;
   int vl_P, vl_K;  // the chunked walk: planes per XCD group, slices per plane (0: natural)
+  // the walk's per-slice-form slices are many enough (cgx_abi.cpp
+  // build_lean_layout) to copy the value dictionary and the templates to LDS
+  // before it; else they read them where they lie (no barrier at the start)
+  int vl_lds;
+  // CSR-stream block visit order (cgx_abi.cpp build_block_order): walk
+  // position -> row block, a permutation within each XCD eighth (null: natural)
+  const int *__restrict__ rbo;
 };
+
+// the row block at walk position `pos` of the CSR-stream forms
+__device__ __forceinline__ int block_at(const CsrArgs &A, int pos) {
+  return A.rbo ? A.rbo[pos] : pos;
+}
 
 // Tile geometry of a variant: bit 64 selects half tiles (1024 entries /
 // 128 rows per row block) — fewer registers per thread, more workgroups per
@@ -489,7 +501,8 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
   const int t = threadIdx.x;
   int first, step, end;
   work_range<V>(A.nrb, first, step, end);
-  for (int b = first; b < end; b += step) {
+  for (int bp = first; bp < end; bp += step) {
+    const int b = block_at(A, bp);
     const int r0 = A.rb[b], r1 = A.rb[b + 1];
     const int nrows = r1 - r0;
     for (int i = t; i <= nrows; i += kBlock) sm.rp[i] = A.rowptr[r0 + i];
@@ -596,7 +609,8 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
   int b, step, end;
   work_range<V>(A.nrb, b, step, end);
   if (b >= end) return;
-  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  const int b0 = block_at(A, b);
+  int r0 = A.rb[b0], r1 = A.rb[b0 + 1], k0 = A.rbk[b0], k1 = A.rbk[b0 + 1];
   PV v[U];
   Int2 c[U];
   auto issue = [&](int kk0, int kk1, PV(&vv)[U], Int2(&cc)[U]) {
@@ -616,7 +630,7 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
   for (;;) {
     const int nb = b + step;
     const bool has_next = nb < end;
-    const int nbb = has_next ? nb : b;
+    const int nbb = block_at(A, has_next ? nb : b);
     const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
     const int nrows = r1 - r0, cnt = k1 - k0;
     const int tr = min(t, max(nrows - 1, 0));
@@ -707,7 +721,8 @@ __device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__rest
   int b, step, end;
   work_range<V>(A.nrb, b, step, end);
   if (b >= end) return;
-  int r0 = A.rb[b], r1 = A.rb[b + 1], k0 = A.rbk[b], k1 = A.rbk[b + 1];
+  const int b0 = block_at(A, b);
+  int r0 = A.rb[b0], r1 = A.rb[b0 + 1], k0 = A.rbk[b0], k1 = A.rbk[b0 + 1];
   QV v[U];
   Int4 c[U];
   auto issue = [&](int kk0, int kk1, QV(&vv)[U], Int4(&cc)[U]) {
@@ -732,7 +747,7 @@ __device__ __forceinline__ void spmv_rows_quad(const CsrArgs &A, const T *__rest
   for (;;) {
     const int nb = b + step;
     const bool has_next = nb < end;
-    const int nbb = has_next ? nb : b;
+    const int nbb = block_at(A, has_next ? nb : b);
     const int nr0 = A.rb[nbb], nr1 = A.rb[nbb + 1], nk0 = A.rbk[nbb], nk1 = A.rbk[nbb + 1];
     const int nrows = r1 - r0, cnt = k1 - k0;
     const int tr = min(t, max(nrows - 1, 0));
@@ -1705,7 +1720,6 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
       A.vl_cls + (int64_t)((A.rev ? 8 * step : 0) + g * step + w) * A.vl_nst);
   const int nw = A.vl_nst >> 2;  // class words of this wave's row
   const auto *tab = (const __attribute__((address_space(4))) VlClass *)A.vl_tab;
-  const int nxm1 = (int)A.nx - 1;
   const unsigned oD = (unsigned)A.vl_D * (unsigned)sizeof(T);
   const unsigned oa = (unsigned)A.vl_a * (unsigned)sizeof(T);
   unsigned cw = 0;
@@ -1724,10 +1738,26 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
     }
     return cb >= K ? end : lo + zp * K + cb + w;
   };
+  const int D = A.vl_D, a = A.vl_a;
+  const int nxi = (int)A.nx;
+  // the +-D carry: when the wave's next slice is the one a plane on (walk
+  // position s + Kp: the plane-matched step, or the chunked walk inside a
+  // chunk), the pair this slice gathers a plane ahead is that slice's center
+  // and this slice's center is its pair a plane behind, so neither is loaded
+  // again (in the reversed sweep "ahead" is -D)
+  const int Kp = D / (2 * kSellRows);
+  const bool carry_walk = D % (2 * kSellRows) == 0 && (P > 0 ? K == Kp : step == Kp);
+  using PV = decltype(x.pair_b(0u));
+  PV c_ahead, c_ct;
+  int carry_s = -1;  // the walk position the carried pairs belong to
   for (int s = lo + w, j = 0; s < end; s = next(s), ++j) {
     if ((j & 255) == 0) {  // the classes of the next 256 steps, lane l: steps 4l .. 4l + 3
       const int k = (j >> 2) + lane;
       cw = k < nw ? row[k] : ~0u;
+      // waited for here (an asm use), and from here on a plain register: the
+      // loop's other iterations do not wait on the memory counter for it
+      // (which would also drain the previous slice's Ap store)
+      asm volatile("" : "+v"(cw));
     }
     const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, (j & 255) >> 2);
     const int c = (int)((word >> (8 * (j & 3))) & 0xffu);
@@ -1736,22 +1766,39 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
       sellpv_slice2<T, VG, Epi, Gather>(A, x, epi, vd, si, vt);
       continue;
     }
-    const int pres = tab[c].pres;
-    const int r0 = si * (2 * kSellRows) + 2 * lane;
-    const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
-    const auto ct = x.pair_b(rb);
-    const auto gmD = x.pair_b(rb - ((pres & 1) ? oD : 0u));
-    const auto gma = x.pair_b(rb - ((pres & 2) ? oa : 0u));
-    const auto gpa = x.pair_b(rb + ((pres & 4) ? oa : 0u));
-    const auto gpD = x.pair_b(rb + ((pres & 8) ? oD : 0u));
+    // every load of the slice at once, none of them waiting on another: the
+    // gathers' addresses follow the slice's position (in bounds, else the
+    // center), not its class, whose presence bits only select the adds
     const int fr = si * (2 * kSellRows);
     const T elo = x.at_s(fr > 0 ? fr - 1 : 0);
-    const T ehi = x.at_s(fr + 2 * kSellRows <= nxm1 ? fr + 2 * kSellRows : nxm1);
+    const T ehi = x.at_s(fr + 2 * kSellRows < nxi ? fr + 2 * kSellRows : nxi - 1);
+    const int r0 = fr + 2 * lane;
+    const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
+    const unsigned omD = rb - (fr >= D ? oD : 0u);
+    const unsigned opD = rb + (fr + 2 * kSellRows + D <= nxi ? oD : 0u);
+    PV ct, behind;
+    if (s == carry_s) {
+      ct = c_ahead;
+      behind = c_ct;
+    } else {
+      ct = x.pair_b(rb);
+      behind = x.pair_b(A.rev ? opD : omD);
+    }
+    const PV ahead = x.pair_b(A.rev ? omD : opD);
+    const auto gma = x.pair_b(rb - (a > 0 && fr >= a ? oa : 0u));
+    const auto gpa = x.pair_b(rb + (a > 0 && fr + 2 * kSellRows + a <= nxi ? oa : 0u));
+    const PV gmD = A.rev ? ahead : behind;
+    const PV gpD = A.rev ? behind : ahead;
+    c_ahead = ahead;
+    c_ct = ct;
+    carry_s = carry_walk ? s + Kp : -1;
+    const int pres = tab[c].pres;
     T v[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) v[q] = T(tab[c].v[q]);
-    const T lo_e = tab[c].plo ? elo : T(tab[c].zlo);
-    const T hi_e = tab[c].phi ? ehi : T(tab[c].zhi);
+    // an absent x-line end: v * (-copysign(0, v)) = -0.0, the identity of +
+    const T lo_e = tab[c].plo ? elo : -__builtin_copysign(T(0), v[2]);
+    const T hi_e = tab[c].phi ? ehi : -__builtin_copysign(T(0), v[4]);
     const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
     epi.pre2c(r0, r0 + 1, ct.x, ct.y);
     T a0 = T(0), a1 = T(0);
@@ -2059,18 +2106,31 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
 }
 
 // k_spmv_dot in the lean stencil walk (kVL): the same epilogue and partials
+// the lean walk's LDS copy of the value dictionary and the templates (a
+// uniform branch: every thread of the workgroup takes it or none)
+template <typename T>
+__device__ __forceinline__ void lean_lds(const CsrArgs &A, SellLds<T> &sm) {
+  const T *__restrict__ src = static_cast<const T *>(A.svdict);
+  for (int i = threadIdx.x; i < kVcDict; i += kBlock) sm.vdict[i] = src[i];
+  for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) sm.vt[i] = A.vct[i];
+  __syncthreads();
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_spmv_lean(CsrArgs A, const T *__restrict__ p,
                                                       T *__restrict__ Ap, CgScalars<T> *st,
                                                       int slot, RedWs<T> *ws) {
   if (!st->active[slot]) return;
   __shared__ SellLds<T> sm;
-  const T *__restrict__ src = static_cast<const T *>(A.svdict);
-  for (int i = threadIdx.x; i < kVcDict; i += kBlock) sm.vdict[i] = src[i];
-  for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) sm.vt[i] = A.vct[i];
-  __syncthreads();
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
-  spmv_lean<T>(A, GatherX<T>{p}, e, sm.vdict, sm.vt);
+  spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
@@ -2221,13 +2281,16 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
       st->rxr[slot] = rr;
     }
   }
-  const T *__restrict__ src = static_cast<const T *>(A.svdict);
-  for (int i = threadIdx.x; i < kVcDict; i += kBlock) sm.vdict[i] = src[i];
-  for (int i = threadIdx.x; i < A.nvt * 64; i += kBlock) sm.vt[i] = A.vct[i];
-  __syncthreads();
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
   const GatherP<T> g{r, pold, beta};
   EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
-  spmv_lean<T>(A, g, e, sm.vdict, sm.vt);
+  spmv_lean<T>(A, g, e, vd, vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
@@ -2886,6 +2949,7 @@ inline CsrArgs args(const CsrDev &A) {
     a.nvt = A.nvt;
   }
   a.col16 = A.col16;
+  a.rbo = A.rbo;
   if (vl_active(A)) {
     a.vl_cls = A.vl_cls;
     a.vl_tab = A.vl_tab;
@@ -2894,6 +2958,7 @@ inline CsrArgs args(const CsrDev &A) {
     a.vl_a = A.vl_a;
     a.vl_P = A.vl_P;
     a.vl_K = A.vl_K;
+    a.vl_lds = A.vl_lds;
   }
   return a;
 }

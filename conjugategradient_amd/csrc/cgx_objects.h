@@ -161,6 +161,7 @@ struct cgx_csr {
   void *d_sell_sl_t = nullptr, *d_vct = nullptr;       // value-code templates (kVT)
   int64_t vt_slices = 0;                               // slices that read a template
   void *d_col16 = nullptr;  // CSR-stream 16-bit column deltas (cgx::CsrDev::col16)
+  void *d_rbo = nullptr;    // CSR-stream block visit order (cgx::CsrDev::rbo)
   // lean stencil walk (kVL, cgx_abi.cpp build_lean): per-slice classes in
   // slice order (host), their device layout for grid dev.vl_grid, the table
   std::vector<int> sell_pool;               // the SELL-P pattern pool (host copy)

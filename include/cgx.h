@@ -78,6 +78,18 @@ int cgx_csr_info(cgx_csr *csr, int64_t *n, int64_t *nnz, int64_t *row_blocks,
 /* Rebuild the SpMV schedule for row blocks of `tile` entries (2048, the
  * default, or 1024 with at most 128 rows). Blocking. */
 int cgx_csr_set_tile(cgx_csr *csr, int tile);
+/* CSR-stream's row-block visit order. A matrix from a 3-D grid gathers p one
+ * plane (D rows) away from every row; walking chunks of `chunk_rows` rows of a
+ * plane through the planes of each XCD's eighth keeps those p lines in the
+ * XCD's L2. chunk_rows: 0 the natural order, -1 automatic (an order only
+ * where a dominant offset D makes two planes of stream overflow half an L2),
+ * > 0 that chunk (CGX_EINVAL without a dominant offset). The result is the
+ * same for any order; only the p.Ap partials group differently. Blocking.
+ * Replaces nothing in the reference: a schedule of VectorOperations.hpp:
+ * 438-466's SpMV. */
+int cgx_csr_set_block_order(cgx_csr *csr, int chunk_rows);
+/* The order in use: the plane offset D and the chunk rows (0 / 0: natural). */
+int cgx_csr_block_order_info(cgx_csr *csr, int *D, int *chunk_rows);
 /* SpMV variant the matrix's launches use: the one cgx_csr_create picked by
  * timing the candidate kernels on the device ($CGX_SPMV_VARIANT or
  * cgx_csr_set_variant override), resolved against the matrix's layout
@@ -99,7 +111,7 @@ int cgx_csr_set_sell(cgx_csr *csr, int rows_per_lane);
 int cgx_csr_sell_info(cgx_csr *csr, int *has_sell, int64_t *padded_entries);
 /* The SELL walk's slice visit order: 1 when the slices are walked in
  * XCD-local chunks of z-planes (automatic where planes span >= 1,024
- * slices; $CGX_SELL_ORDER), 2 when a partitioned matrix's interior slice
+ * slices), 2 when a partitioned matrix's interior slice
  * list is, 0 for the natural order. */
 int cgx_csr_visit_order(cgx_csr *csr, int *ordered);
 /* Distinct values of the matrix's SELL-P value codes (variant bit 32768:
@@ -128,7 +140,7 @@ int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, in
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D
  * a multiple of 128 rows, and the bit is ignored), *offset_a = the 3-D
  * form's +-a offset (0: 2-D form), *run_planes = planes per run (0: chosen
- * per launch to fill the grid; $CGX_MARCH_LEN sets it). */
+ * per launch to fill the grid). */
 int cgx_csr_march_info(cgx_csr *csr, int *stride, int *offset_a, int *run_planes);
 /* Bytes of the matrix stream one SpMV launch in the matrix's current
  * variant reads (values, indices / codes / masks, slice descriptors;

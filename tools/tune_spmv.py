@@ -5,6 +5,8 @@ one process (cdna_hip_programming.md §5.4 rule 24). Prints one JSON line per
 y against variant 0 bit for bit.
 
     python tools/tune_spmv.py [--configs 3d256,2d4096,irr] [--rounds 5] [--iters 20]
+                              [--orders 0,-1,2048]   (CSR-stream block orders,
+                              cgx_csr_set_block_order's chunk rows)
 """
 from __future__ import annotations
 
@@ -46,10 +48,12 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--orders", default="")
     a = ap.parse_args()
     L = lib()
     q = cga.Queue(0)
     variants = [int(v) for v in a.variants.split(",")]
+    orders = [int(o) for o in a.orders.split(",")] if a.orders else [None]
     if any(v & 2048 for v in variants):  # keep the SELL-64 copy (autotune may free it)
         os.environ.setdefault("CGX_SPMV_VARIANT", "2048")
     for name in a.configs.split(","):
@@ -71,22 +75,30 @@ def main():
                                    A.data().ptr, 0, None, C.byref(pair)))
             check(L.cgx_csr_set_sell(pair, 2))
         x = cga.Vector(q, np.random.default_rng(0).standard_normal(n))
-        ys = {v: cga.Vector(q, n) for v in variants}
-        times = {v: [] for v in variants}
+        keys = [(v, o) for v in variants for o in orders]
+        ys = {k: cga.Vector(q, n) for k in keys}
+        times = {k: [] for k in keys}
+        used = {}
         for _ in range(a.rounds):
-            for v in variants:
+            for v, o in keys:
                 ms = C.c_double(0)
                 sched = (pair if v & 4096 else wave if v & 512 else half if v & 64
                          else A.schedule())
-                check(L.cgx_tune_spmv(q.handle, sched, v, x.ptr(), ys[v].ptr(), a.iters,
+                if o is not None:
+                    check(L.cgx_csr_set_block_order(sched, o))
+                    d, w = C.c_int(), C.c_int()
+                    check(L.cgx_csr_block_order_info(sched, C.byref(d), C.byref(w)))
+                    used[(v, o)] = [d.value, w.value]
+                check(L.cgx_tune_spmv(q.handle, sched, v, x.ptr(), ys[(v, o)].ptr(), a.iters,
                                       C.byref(ms)))
-                times[v].append(ms.value)
-        y0 = ys[variants[0]].to_numpy()
+                times[(v, o)].append(ms.value)
+        y0 = ys[keys[0]].to_numpy()
         nbytes = 12 * nnz + 4 * (n + 1) + 16 * n
-        for v in variants:
-            t = np.array(times[v]) * 1e3
-            same = bool(np.array_equal(ys[v].to_numpy(), y0))
-            print(json.dumps({"config": name, "variant": v, "n": n, "nnz": nnz,
+        for v, o in keys:
+            t = np.array(times[(v, o)]) * 1e3
+            same = bool(np.array_equal(ys[(v, o)].to_numpy(), y0))
+            print(json.dumps({"config": name, "variant": v, "order": used.get((v, o)),
+                              "n": n, "nnz": nnz,
                               "median_us": round(float(np.median(t)), 2),
                               "min_us": round(float(t.min()), 2),
                               "GBps_median": round(nbytes / (np.median(t) * 1e-6) / 1e9, 1),
