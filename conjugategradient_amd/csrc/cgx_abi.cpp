@@ -41,7 +41,8 @@ int hip_fail(hipError_t e, const char *what) {
   return CGX_EHIP;
 }
 
-std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz, int tile) {
+std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz, int tile,
+                                  const std::vector<int64_t> *cuts) {
   const int cap = tile - 6;                            // quad loads (kTileCap)
   const int rows_max = tile / 8;  // 2048 -> 256, 1024 -> 128, 512 -> 64 rows
   std::vector<int> rb;
@@ -49,15 +50,19 @@ std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz
   rb.push_back(0);
   int64_t row = 0;
   int mx = 0;
+  size_t ci = 0;
   while (row < n) {
     const int64_t start = row;
+    // the next cut after this block's first row: the block ends before it
+    while (cuts && ci < cuts->size() && (*cuts)[ci] <= start) ++ci;
+    const int64_t lim = (cuts && ci < cuts->size()) ? (*cuts)[ci] : n;
     int len = rowptr[row + 1] - rowptr[row];
     if (len > cap) {  // a long row gets a workgroup of its own
       mx = std::max(mx, len);
       ++row;
     } else {
       int64_t acc = 0;
-      while (row < n && row - start < rows_max) {
+      while (row < lim && row - start < rows_max) {
         len = rowptr[row + 1] - rowptr[row];
         if (acc + len > cap) break;
         acc += len;
@@ -173,32 +178,43 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
     // slices, one launch less)
     const bool split = A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192));
     const int wg0 = A->peer.dev.nsend * kPushWG;
-    const bool merged = split && wg0 > 0 && Launch<T>::push_supported(A->dev);
+    // the interior slices by the lean walk (its layout skips the boundary ones)
+    const bool lean_in = split && vl_active(A->dev) && A->dev.vl_split;
+    const bool merged = split && wg0 > 0 && (lean_in || Launch<T>::push_supported(A->dev));
     // (the wait stays a launch of its own: round 2's folded form had the
     // boundary workgroups spin on flags raised by the same launch's first
     // workgroups, which relies on their being resident; removed in round 3,
     // DESIGN.md §9)
     if (!merged && (rc = peer_push<T>(A, p, st, slot, s))) return rc;
-    const int gi = !split ? 0
-                   : merged ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
-                            : Launch<T>::slice_grid(A->dev, A->split_ni);
+    const int gi = !split  ? 0
+                   : lean_in ? A->dev.vl_grid
+                   : merged  ? Launch<T>::slice_grid_push(A->dev, A->split_ni, wg0)
+                             : Launch<T>::slice_grid(A->dev, A->split_ni);
     // the boundary slices wait for the neighbours' pushes themselves and read
     // the ghosts from the landing buffer (k_spmv_dot_bnd): no k_peer_wait
     // launch, no copy into p's ghost tail (matrices without the split keep
     // k_peer_wait before their one launch)
-    const bool fold = split && A->split_nb > 0 && Launch<T>::bnd_supported(A->dev);
+    // the boundary rows run as CSR-stream blocks (their own entry order; the
+    // SELL copy holds them only as placeholders) with the wait folded in
+    const bool rows = split && A->bnd_nblk > 0;
+    const bool fold = split && A->split_nb > 0 && (rows || Launch<T>::bnd_supported(A->dev));
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = hipSuccess;
-           if (merged)
+           if (lean_in)
+             e = Launch<T>::spmv_lean_interior(A->dev, p, Ap, st, slot, ws, s, rev,
+                                               merged ? &A->peer.dev : nullptr, wg0);
+           else if (merged)
              e = Launch<T>::spmv_dot_slices_push(A->dev, A->d_split, A->split_ni, 0, p, Ap, st,
                                                  slot, ws, s, rev, A->peer.dev, wg0);
            else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
            if (e == hipSuccess && fold)
-             return Launch<T>::spmv_dot_slices_bnd(A->dev, A->d_split + A->split_ni,
-                                                   A->split_nb, gi, p, Ap, st, slot, ws, s, rev,
-                                                   A->peer.dev);
+             return rows ? Launch<T>::spmv_dot_rows(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, p, Ap,
+                                                    st, slot, ws, s, &A->peer.dev)
+                         : Launch<T>::spmv_dot_slices_bnd(A->dev, A->d_split + A->split_ni,
+                                                          A->split_nb, gi, p, Ap, st, slot, ws, s,
+                                                          rev, A->peer.dev);
            if (e == hipSuccess && peer_wait<T>(A, p, st, slot, s)) e = hipErrorLaunchFailure;
            if (e == hipSuccess)
              e = split ? Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,
@@ -207,25 +223,35 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            return e;
          })))
       return rc;
-    *np = !split ? Launch<T>::spmv_parts(A->dev) : gi + Launch<T>::slice_grid(A->dev, A->split_nb);
+    *np = !split ? Launch<T>::spmv_parts(A->dev)
+                 : gi + (rows ? Launch<T>::rows_grid(A->dev, A->bnd_nblk)
+                              : Launch<T>::slice_grid(A->dev, A->split_nb));
     return CGX_OK;
   }
   if (halo && A->split_ni > 0 && (launch_variant(A->dev, A->dtype) & (2048 | 8192))) {
     bool async = false;
     if ((rc = dist_halo_post(A, p, s, &async))) return rc;
-    const int gi = Launch<T>::slice_grid(A->dev, A->split_ni);
+    const bool lean_in = vl_active(A->dev) && A->dev.vl_split;
+    const bool rows = A->bnd_nblk > 0;
+    const int gi = lean_in ? A->dev.vl_grid : Launch<T>::slice_grid(A->dev, A->split_ni);
     // one timed region: interior slices, the wait for the halo, boundary slices
     if ((rc = timed(cg, 1, s, [&] {
-           hipError_t e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap,
-                                                     st, slot, ws, s, rev);
+           hipError_t e =
+               lean_in ? Launch<T>::spmv_lean_interior(A->dev, p, Ap, st, slot, ws, s, rev,
+                                                       nullptr, 0)
+                       : Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap,
+                                                    st, slot, ws, s, rev);
            if (e == hipSuccess && async) e = hipStreamWaitEvent(s, A->ev_halo, 0);
            if (e == hipSuccess)
-             e = Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb, gi, p,
-                                            Ap, st, slot, ws, s, rev);
+             e = rows ? Launch<T>::spmv_dot_rows(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, p, Ap, st,
+                                                 slot, ws, s, nullptr)
+                      : Launch<T>::spmv_dot_slices(A->dev, A->d_split + A->split_ni, A->split_nb,
+                                                   gi, p, Ap, st, slot, ws, s, rev);
            return e;
          })))
       return rc;
-    *np = gi + Launch<T>::slice_grid(A->dev, A->split_nb);
+    *np = gi + (rows ? Launch<T>::rows_grid(A->dev, A->bnd_nblk)
+                     : Launch<T>::slice_grid(A->dev, A->split_nb));
     return CGX_OK;
   }
   if (halo && (rc = dist_halo_exchange(A, p, s))) return rc;
@@ -326,9 +352,9 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
 // Fused deferred-x iteration (mode 4, single device): two kernels per body.
 // Kernel 1 computes p_k = r + beta p_{k-1} where the SpMV reads it and
 // stores it into P[k mod 4] (no separate p update: one read of p less per
-// body), kernel 2 is update_r with the stop rule; in slot 3 the group's x
-// updates are applied from the four p buffers (k_flush_group). Same values
-// as modes 1 and 3, bit for bit.
+// body), kernel 2 is update_r with the stop rule; in slot 3 it also applies
+// the group's x updates from the four p buffers (k_update_r_flush). Same
+// values as modes 1 and 3, bit for bit.
 template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
   cgx_csr *A = cg->A;
   hipStream_t s = cg->ctx->stream;
@@ -345,12 +371,14 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
                                    s, par);
        })))
     return rc;
+  // kernel 2: update_r with the stop rule; in slot 3 it also applies the
+  // group's deferred x updates (one launch instead of a separate flush)
   if ((rc = timed(cg, 2, s, [&] {
-         return Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, npp, rpar, nullptr, 1);
+         return slot == 3 ? Launch<T>::update_r_flush(cg->n, r, Ap, st, slot, ws, npp, rpar, x, P,
+                                                      s)
+                          : Launch<T>::update_r(cg->n, r, Ap, st, slot, ws, s, false, npp, rpar,
+                                                nullptr, 1);
        })))
-    return rc;
-  if (slot == 3 &&
-      (rc = timed(cg, 3, s, [&] { return Launch<T>::flush_group(cg->n, x, P, st, s, rpar); })))
     return rc;
   return CGX_OK;
 }
@@ -776,7 +804,8 @@ extern "C" int cgx_fill(cgx_ctx *ctx, int dtype, void *d, double v, size_t n) {
 }
 
 int autotune_spmv(cgx_csr *A);
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0,
+               const std::vector<char> *skip = nullptr);
 int build_value_codes(cgx_csr *A);
 void free_sell(cgx_csr *A);
 
@@ -1073,7 +1102,8 @@ void free_lean(cgx_csr *A) {
   A->dev.vl_cls = nullptr;
   A->dev.vl_tab = nullptr;
   A->dev.vl_grid = A->dev.vl_nst = A->dev.vl_D = A->dev.vl_a = 0;
-  A->dev.vl_P = A->dev.vl_K = A->dev.vl_lds = 0;
+  A->dev.vl_P = A->dev.vl_K = A->dev.vl_lds = A->dev.vl_split = 0;
+  A->vl_tab_h.clear();
   A->dev.lean = false;
   A->vl_slice_cls.clear();
   A->vl_ncls = 0;
@@ -1105,6 +1135,10 @@ void free_sell(cgx_csr *A) {
   A->dev.nvt = 0;
   A->vt_slices = 0;
   A->split_ni = A->split_nb = 0;
+  if (A->d_bnd_blk) (void)hipFree(A->d_bnd_blk);
+  A->d_bnd_blk = nullptr;
+  A->bnd_nblk = 0;
+  A->dev.sell_partial = 0;
   A->dev.sell_r = 1;
   A->dev.sell_maxw = 0;
   A->dev.march_k = A->dev.march_a = A->dev.march_len = 0;
@@ -1191,9 +1225,12 @@ static bool sell_plan_host(int64_t n, const int *rowptr, const int *col, int R,
 // union of its (col - row) offsets, at most kSellPatMax; rows must have
 // strictly ascending columns (then a row's set slots are its CSR order).
 // Padding bound as in sell_plan_host. maxw: the widest pattern.
+// skip: slices that hold placeholders (a partitioned matrix's boundary
+// slices, never run in this layout), exempt from the sorted-rows rule.
 static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
                             std::vector<SellSlice> &sl, std::vector<int> &pool,
-                            int64_t &voff_total, int &maxw) {
+                            int64_t &voff_total, int &maxw,
+                            const std::vector<char> *skip = nullptr) {
   const int64_t nnz = (int64_t)rowptr[n] - rowptr[0];
   const int64_t H = 2 * kSellRows;
   if (nnz < 1 || n + H >= (int64_t(1) << 31)) return false;
@@ -1209,7 +1246,9 @@ static bool sellp_plan_host(int64_t n, const int *rowptr, const int *col,
     P.clear();
     for (int64_t i = r0; i < r1; ++i) {
       for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-        if (k > rowptr[i] && col[k] <= col[k - 1]) return false;  // unsorted or duplicate
+        if (k > rowptr[i] && col[k] <= col[k - 1] &&
+            !(skip && (size_t)q < skip->size() && (*skip)[(size_t)q]))
+          return false;  // unsorted or duplicate
         const int off = col[k] - (int)i;
         auto it = std::lower_bound(P.begin(), P.end(), off);
         if (it == P.end() || *it != off) {
@@ -1569,7 +1608,7 @@ static int build_lean_classes(cgx_csr *A, std::vector<VlClass> &tab) {
   tab.clear();
   A->vl_slice_cls.clear();
   const CsrDev &d = A->dev;
-  if (A->dist || !d.sl_t || !d.vct || d.nvt < 1 || !d.svc4 || !d.svdict || d.sell_maxw > 8 ||
+  if (!d.sl_t || !d.vct || d.nvt < 1 || !d.svc4 || !d.svdict || d.sell_maxw > 8 ||
       A->sell_pool.empty() || (uint64_t)(d.n + 2) * dtype_size(A->dtype) >= (uint64_t(1) << 32))
     return CGX_OK;
   hipStream_t s = A->ctx->stream;
@@ -1775,6 +1814,7 @@ static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G)
   for (unsigned char c : A->vl_slice_cls) generic += c == 0xff;
   A->dev.vl_lds = generic >= 64 ? 1 : 0;
   A->vl_ncls = (int)tab.size();
+  A->vl_tab_h = tab;
   return CGX_OK;
 }
 
@@ -1807,6 +1847,22 @@ static bool build_lean(cgx_csr *A, int G = 0) {
   if (G == 0) G = lean_grid(A);
   return build_lean_layout(A, tab, G) == CGX_OK;
 }
+// A partitioned matrix whose loop SpMV is the lean walk: its boundary slices
+// (the split's, run by the boundary launch with the ghosts) become class
+// 0xfe, skipped by the walk, and the layout is rebuilt at the same grid; the
+// walk then runs the interior slices (spmv_lean_interior). Boundary slices
+// never take the whole-matrix walk (vl_whole).
+int lean_mark_split(cgx_csr *A, const std::vector<int> &boundary) {
+  if (!A->dev.lean || A->vl_slice_cls.empty() || A->vl_tab_h.empty() || boundary.empty())
+    return CGX_OK;
+  for (int q : boundary)
+    if (q >= 0 && (size_t)q < A->vl_slice_cls.size()) A->vl_slice_cls[(size_t)q] = 0xfe;
+  const std::vector<VlClass> tab = A->vl_tab_h;
+  if (int rc = build_lean_layout(A, tab, A->dev.vl_grid)) return rc;
+  A->dev.vl_split = 1;
+  return CGX_OK;
+}
+
 // the variant under the lean walk: its generic slices' form (4-bit value
 // codes on templates, the pipelined stencil walk's requirements)
 constexpr int kVlBase = 2050 | 32768 | 262144 | 524288 | 1048576 | kVT;
@@ -1822,7 +1878,8 @@ int build_value_codes(cgx_csr *A) {
 // when the matrix qualifies (sell_plan_host); otherwise A keeps only the
 // CSR-stream schedule and this returns CGX_OK. Errors are device failures
 // only. cgx_csr_set_sell selects R (0 drops the copy).
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R,
+               const std::vector<char> *skip) {
   // R: 1 / 2 dictionary SELL with R rows per lane, 3 SELL-P (2 rows per
   // lane), 0 the default: SELL-P where the matrix qualifies, else R = 2
   bool fallback = false;
@@ -1857,7 +1914,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   int kind = 0, maxw = 0;
   const int64_t nx = A->dev.n + A->halo.n_ghost;
   if (R == 3) {
-    if (nx >= 2 && sellp_plan_host(n, h_rowptr, h_col, sl, pool, voff, maxw)) {
+    if (nx >= 2 && sellp_plan_host(n, h_rowptr, h_col, sl, pool, voff, maxw, skip)) {
       kind = maxw <= 8 ? 1 : 2;
       R = 2;
     } else if (fallback) {
@@ -1915,6 +1972,7 @@ int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R = 0) {
   }
   A->dev.sl = (const SellSlice *)A->d_sell_sl;
   A->dev.sdict = (const int *)A->d_sell_dict;
+  A->dev.sell_partial = (kind && skip) ? 1 : 0;
   A->sell_pool = pool;
   A->dev.sidx = (const unsigned long long *)A->d_sell_idx;
   A->dev.sval = A->d_sell_val;
@@ -2013,7 +2071,7 @@ extern "C" int cgx_csr_lean_info(cgx_csr *A, int *classes, int64_t *slices, int 
   const bool on = A->dev.vl_cls != nullptr;
   int64_t cnt = 0;
   if (on)
-    for (unsigned char c : A->vl_slice_cls) cnt += c != 0xff;
+    for (unsigned char c : A->vl_slice_cls) cnt += c < 0xfe;  // 0xff / 0xfe: not lean
   *classes = on ? A->vl_ncls : 0;
   *slices = cnt;
   *grid = on ? A->dev.vl_grid : 0;

@@ -27,7 +27,9 @@
 #include "cgx_objects.h"
 
 int autotune_spmv(cgx_csr *A);  // cgx_abi.cpp
-int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R);
+int build_sell(cgx_csr *A, const int *h_rowptr, const int *h_col, int R,
+               const std::vector<char> *skip);
+int lean_mark_split(cgx_csr *A, const std::vector<int> &boundary);  // cgx_abi.cpp
 std::vector<int> chunked_slice_order(const std::vector<int> &ids, int64_t H, int64_t P,
                                      int64_t kChunk);  // cgx_abi.cpp
 
@@ -592,9 +594,23 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     return rc;
   }
   e = hipMemcpyAsync(d_col, hcol.data(), hcol.size() * sizeof(int), hipMemcpyHostToDevice, s);
-  // 6. SpMV schedule over the local rows (+ entry offsets)
+  // 6. boundary rows (any ghost column) in 128-row slices (the SELL-P
+  // slice), and the SpMV schedule over the local rows (+ entry offsets), cut
+  // at the ends of the boundary runs so its blocks lie inside or outside them
+  const int64_t HS = 2 * kSellRows;
+  const int64_t nsl_b = (n_local + HS - 1) / HS;
+  std::vector<char> bslice((size_t)nsl_b, 0);
+  for (int64_t r = 0; r < n_local; ++r)
+    for (int64_t k = hrp[(size_t)r]; k < hrp[(size_t)r + 1]; ++k)
+      if (hcol[(size_t)k] >= n_local) {
+        bslice[(size_t)(r / HS)] = 1;
+        break;
+      }
+  std::vector<int64_t> cuts;
+  for (int64_t q = 0; q < nsl_b; ++q)
+    if (bslice[(size_t)q] != (q > 0 ? bslice[(size_t)q - 1] : 0)) cuts.push_back(q * HS);
   int mx = 0;
-  std::vector<int> rb = build_row_blocks(hrp.data(), n_local, &mx);
+  std::vector<int> rb = build_row_blocks(hrp.data(), n_local, &mx, kTile, &cuts);
   const size_t nrb1 = rb.size();
   rb.resize(2 * nrb1);
   for (size_t i = 0; i < nrb1; ++i) rb[nrb1 + i] = hrp[rb[i]];
@@ -609,7 +625,11 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   A->max_row_nnz = mx;
   A->dev = CsrDev{n_local, nnz_local, d_rowptr, d_col, d_val, A->d_rb, A->d_rb + nrb1,
                   (int)nrb1 - 1, kTile};
-  if ((rc = build_sell(A, hrp.data(), hcol.data(), 0)) || (rc = autotune_spmv(A))) {
+  // the boundary slices are placeholders in the SELL copy (their rows may be
+  // unsorted locally: ghosts from lower ranks are numbered after the own
+  // rows); the boundary launch runs their rows as CSR-stream blocks
+  if ((rc = build_sell(A, hrp.data(), hcol.data(), 0, h.n_ghost > 0 ? &bslice : nullptr)) ||
+      (rc = autotune_spmv(A))) {
     cgx_csr_destroy(A);
     return rc;
   }
@@ -620,10 +640,9 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     const int64_t H = (int64_t)kSellRows * A->dev.sell_r, nsl = A->dev.nsl;
     std::vector<int> in, bd;
     for (int64_t q = 0; q < nsl; ++q) {
-      const int64_t r0 = q * H, r1 = std::min<int64_t>(n_local, r0 + H);
-      bool ghost = false;
-      for (int64_t k = hrp[(size_t)r0]; k < hrp[(size_t)r1] && !ghost; ++k)
-        ghost = hcol[(size_t)k] >= n_local;
+      // boundary: inside a 128-row run that holds a ghost column (the rows
+      // the boundary launch's CSR blocks cover, so no row runs twice)
+      const bool ghost = bslice[(size_t)(q * H / HS)] != 0;
       (ghost ? bd : in).push_back((int)q);
     }
     // the interior slices in the chunked visit order of a single-device
@@ -658,6 +677,29 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
       }
       A->split_ni = (int)(in.size() - bd.size());
       A->split_nb = (int)bd.size();
+      // the boundary rows' CSR-stream blocks (whole blocks: the schedule is
+      // cut at the runs' ends)
+      std::vector<int> blk;
+      for (int b = 0; b + 1 < (int)nrb1; ++b)
+        if (bslice[(size_t)(rb[(size_t)b] / HS)]) blk.push_back(b);
+      if (!blk.empty()) {
+        e = hipMalloc(&A->d_bnd_blk, blk.size() * sizeof(int));
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(A->d_bnd_blk, blk.data(), blk.size() * sizeof(int),
+                             hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+          cgx_csr_destroy(A);
+          return hip_fail(e, "cgx_csr_create_dist(boundary blocks)");
+        }
+        A->bnd_nblk = (int)blk.size();
+      }
+      // a lean loop SpMV walks the interior only (the boundary slices are the
+      // boundary launch's)
+      if ((rc = lean_mark_split(A, bd))) {
+        cgx_csr_destroy(A);
+        return rc;
+      }
     }
   }
   *out = A;

@@ -191,7 +191,14 @@ struct CsrDev {
   int vl_grid = 0, vl_nst = 0, vl_D = 0, vl_a = 0;
   int vl_P = 0, vl_K = 0;  // the chunked walk's planes per XCD group, slices per plane
   int vl_lds = 0;  // the per-slice form's dictionary and templates copied to LDS first
+  // a partitioned matrix's layout: its boundary slices (the split's, run by
+  // the boundary launch) are skipped, so the walk covers the interior only
+  int vl_split = 0;
   bool lean = false;
+  // a partitioned matrix's SELL copy holds its boundary slices only as
+  // placeholders (their rows may be unsorted in local numbering: ghosts from
+  // lower ranks come after the own rows); whole-matrix SpMVs take CSR-stream
+  int sell_partial = 0;
   // CSR-stream block visit order (cgx_abi.cpp build_block_order; null:
   // natural): walk position -> row block, a permutation within each XCD
   // eighth that walks chunks of ob_W rows through planes ob_D rows apart
@@ -212,6 +219,10 @@ __host__ __device__ inline bool vt_active(const CsrDev &A) {
 // template value-code form, so vt_active holds too)
 __host__ __device__ inline bool vl_active(const CsrDev &A) {
   return A.lean && A.vl_cls && A.vl_tab && A.vl_grid > 0 && vt_active(A);
+}
+// the lean walk covers the whole matrix (not a partitioned matrix's interior)
+__host__ __device__ inline bool vl_whole(const CsrDev &A) {
+  return vl_active(A) && !A.vl_split && !A.sell_partial;
 }
 
 template <typename T> struct Launch {
@@ -246,6 +257,22 @@ template <typename T> struct Launch {
                             hipStream_t s, int rev = 0);
   static hipError_t flush_group(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                 hipStream_t s, int rev = 0);
+  // a partitioned matrix's boundary rows: CSR-stream over the row blocks
+  // `blocks` (count), partials at [part_off, part_off + grid); with P the
+  // ghosts come from the peer landing buffer after the neighbours' pushes
+  static hipError_t spmv_dot_rows(const CsrDev &A, const int *blocks, int count, int part_off,
+                                  const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                  hipStream_t s, const PeerDev *P);
+  static int rows_grid(const CsrDev &A, int count);
+  // a partitioned matrix's interior slices by the lean walk (A.vl_split), the
+  // halo push in the first wg0 workgroups when P is given; partials [0, vl_grid)
+  static hipError_t spmv_lean_interior(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
+                                       int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                       const PeerDev *P, int wg0);
+  // mode 4, slot 3: update_r (stop rule) and the group flush in one launch
+  static hipError_t update_r_flush(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
+                                   RedWs<T> *ws, int np_pap, int rev, T *x, T *const P[4],
+                                   hipStream_t s);
   static hipError_t rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s);
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
@@ -369,8 +396,9 @@ bool launch_variant_ok(const CsrDev &A, int dtype);
 bool spmv_listed(int v);
 
 // host-side row-block schedule (cgx_abi.cpp)
+// cuts: sorted rows no block may straddle (a block ends before each)
 std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz,
-                                  int tile = kTile);
+                                  int tile = kTile, const std::vector<int64_t> *cuts = nullptr);
 
 __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, int64_t row);
 

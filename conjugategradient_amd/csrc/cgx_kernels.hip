@@ -505,11 +505,15 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
     const int b = block_at(A, bp);
     const int r0 = A.rb[b], r1 = A.rb[b + 1];
     const int nrows = r1 - r0;
-    for (int i = t; i <= nrows; i += kBlock) sm.rp[i] = A.rowptr[r0 + i];
-    __syncthreads();
-    const int k0 = sm.rp[0];
-    const int cnt = sm.rp[nrows] - k0;
+    const int k0 = A.rbk[b];
+    const int cnt = A.rbk[b + 1] - k0;
     if (cnt <= TL::cap) {
+      // this thread's row bounds and own operands go out with the block's
+      // entries (none waits on another): two memory round trips per block,
+      // the entries and then the gathers
+      const int tr = min(t, max(nrows - 1, 0));
+      const int ra = A.rowptr[r0 + tr] - k0, re = A.rowptr[r0 + tr + 1] - k0;
+      epi.pre(r0 + tr);
       if (cnt > 0) {
         if constexpr (PAIRS) {
           using PV = typename PairOf<T>::V;
@@ -571,10 +575,8 @@ __device__ __forceinline__ void spmv_rows(const CsrArgs &A, const T *__restrict_
       }
       __syncthreads();
       if (t < nrows) {
-        const int a = sm.rp[t] - k0, e = sm.rp[t + 1] - k0;
-        epi.pre(r0 + t);
         T s = T(0);
-        for (int j = a; j < e; ++j) s += sm.prod[j];
+        for (int j = ra; j < re; ++j) s += sm.prod[j];
         epi.row(r0 + t, s);
       }
       __syncthreads();
@@ -1710,7 +1712,9 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
   constexpr int VG = 8192 | 32768 | 262144 | 524288 | kVT | 2;  // the generic slices' form
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int G = (int)gridDim.x, b = (int)blockIdx.x, g = b & 7;
+  // (the first A.wg0 workgroups of a launch with the halo push do that
+  // instead; a multiple of 8, so the XCD groups stay)
+  const int G = (int)gridDim.x - A.wg0, b = (int)blockIdx.x - A.wg0, g = b & 7;
   const int step = (G >> 3) * 4, w = (b >> 3) * 4 + wid;
   const int nsl = (int)A.nsl;
   const int lo = (int)(((int64_t)nsl * g) >> 3), end = (int)(((int64_t)nsl * (g + 1)) >> 3);
@@ -1762,6 +1766,7 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
     const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, (j & 255) >> 2);
     const int c = (int)((word >> (8 * (j & 3))) & 0xffu);
     const int si = A.rev ? lo + end - 1 - s : s;
+    if (c == 0xfe) continue;  // a partitioned matrix's boundary slice: the boundary launch's
     if (c == 0xff) {
       sellpv_slice2<T, VG, Epi, Gather>(A, x, epi, vd, si, vt);
       continue;
@@ -2133,7 +2138,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean(CsrArgs A, const T *__rest
   spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
 }
 
 // The interior SpMV of a partitioned SELL matrix with the device peer
@@ -2154,6 +2159,33 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
   __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+}
+
+// A partitioned matrix's interior slices by the lean walk (its layout skips
+// the boundary slices) with the halo push in the first A.wg0 workgroups, as
+// k_spmv_dot_push does for the slice-list form
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_lean_push(CsrArgs A, const T *__restrict__ p,
+                                                           T *__restrict__ Ap, CgScalars<T> *st,
+                                                           int slot, RedWs<T> *ws, PeerDev P) {
+  if ((int)blockIdx.x < A.wg0) {
+    peerdev::push_wg<T>(p, P, st, slot, blockIdx.x);
+    return;
+  }
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
+  spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
@@ -2400,12 +2432,77 @@ template <typename T> __device__ __forceinline__ void peer_fault(CgScalars<T> *s
   }
 }
 
-template <typename T, bool FUSED, bool PEER, bool SNT>
+// mode 4's group flush folded into slot 3's update_r: x and the group's p buffers
+template <typename T> struct XFlush {
+  T *x;
+  const T *P[4];
+};
+// Mode 4, slot 3: the group's deferred x updates, x = (((x + a0 p0) + a1
+// p1) + a2 p2) + a3 p3 over the slots whose use[] is set (the slots that ran
+// in this group and no end-of-run flush applied: k_flush_defer's rule;
+// k_spmv_fd of the next slot 0 clears ran[]). 16-byte lanes over this
+// launch's grid; x and the p buffers are not re-read before the next group
+// overwrites them.
+template <typename T>
+__device__ __forceinline__ void flush_group_range(int64_t n, T *__restrict__ x,
+                                                  const T *__restrict__ P0,
+                                                  const T *__restrict__ P1,
+                                                  const T *__restrict__ P2,
+                                                  const T *__restrict__ P3, const T (&a)[4],
+                                                  const bool (&use)[4], int rev) {
+  using V = typename Vec2<T>::V;
+  const int64_t n2 = n >> 1;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  V *x2 = reinterpret_cast<V *>(x);
+  const V *Q[4] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
+                   reinterpret_cast<const V *>(P2), reinterpret_cast<const V *>(P3)};
+  auto body = [&](int64_t i, auto sntc) {
+    constexpr bool S = decltype(sntc)::value;
+    V xv = ldv<S, T>(x2 + i);
+    V q[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) q[t] = ldv<S, T>(Q[t] + i);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (use[t]) {
+        xv.x = xv.x + a[t] * q[t].x;
+        xv.y = xv.y + a[t] * q[t].y;
+      }
+    }
+    stv<S, T>(x2 + i, xv);
+  };
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };
+  auto loop = [&](auto sntc) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + stride < n2; i += 2 * stride) {
+      body(E(i), sntc);
+      body(E(i + stride), sntc);
+    }
+    for (; i < n2; i += stride) body(E(i), sntc);
+  };
+  if (stream_nt<T>(n))
+    loop(std::true_type{});
+  else
+    loop(std::false_type{});
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    T xv = x[n - 1];
+    const T *Ps[4] = {P0, P1, P2, P3};
+    for (int t = 0; t < 4; ++t)
+      if (use[t]) xv = xv + a[t] * Ps[t][n - 1];
+    x[n - 1] = xv;
+  }
+}
+
+
+template <typename T, bool FUSED, bool PEER, bool SNT, bool GF = false>
 // rin == r: in place (modes 1, 2); else r ping-pongs between two buffers.
+// GF (mode 4, slot 3): after r, the group's deferred x updates (xf), also
+// when the body itself is inactive (the group's earlier bodies that ran).
 __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
                                               const T *__restrict__ Ap, CgScalars<T> *st,
                                               int slot, RedWs<T> *ws, int np_pap, int rev,
-                                              int rule, const PeerDev *P) {
+                                              int rule, const PeerDev *P,
+                                              const XFlush<T> *xf = nullptr) {
   // rule (mode 4, kernel 2 of 2): this kernel also runs the stop rule
   // (CG.hpp:396-404, 436: on the r.r the body started with, which k_spmv_fd
   // recorded) and marks the body's x update pending (ran[slot])
@@ -2439,6 +2536,17 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     rv[u] = ri2[j];
     av[u] = ldv<SNT, T>(a2 + j);  // Ap is dead after this kernel
   }
+  // the group flush's alphas and flags of the earlier slots (written by
+  // earlier launches; this one writes only slot 3's)
+  T ga[4] = {T(0), T(0), T(0), T(0)};
+  bool guse[4] = {false, false, false, false};
+  if constexpr (GF) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      ga[t] = cst->alpha[t];
+      guse[t] = cst->ran[t] != 0 && cst->skip[t] == 0;
+    }
+  }
   if (!act) {
     keep(rxr);
     keep(pAp_st);
@@ -2446,6 +2554,10 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     keep(rv);
     keep(av);
     if ((FUSED || rule) && blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
+    if constexpr (GF) {
+      if (guse[0] || guse[1] || guse[2])
+        flush_group_range<T>(n, xf->x, xf->P[0], xf->P[1], xf->P[2], xf->P[3], ga, guse, rev);
+    }
     return;
   }
   T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
@@ -2510,6 +2622,11 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     r[n - 1] = v;
     acc += v * v;
   }
+  if constexpr (GF) {
+    ga[3] = alpha;
+    guse[3] = true;
+    flush_group_range<T>(n, xf->x, xf->P[0], xf->P[1], xf->P[2], xf->P[3], ga, guse, rev);
+  }
   T v[1] = {acc};
   if constexpr (!FUSED) {  // this workgroup's share of r.r; the next kernel sums them
     block_sum<T, 1>(v, red);
@@ -2544,6 +2661,21 @@ __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T 
   else
     update_r_body<T, FUSED, false, false>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule,
                                           nullptr);
+}
+// Mode 4, slot 3: update_r with the stop rule and the group's x flush in one
+// launch (k_flush_group's values, bit for bit)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_update_r_flush(int64_t n, T *r,
+                                                           const T *__restrict__ Ap,
+                                                           CgScalars<T> *st, int slot,
+                                                           RedWs<T> *ws, int np_pap, int rev,
+                                                           XFlush<T> xf) {
+  if (stream_nt<T>(n))
+    update_r_body<T, false, false, true, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, nullptr,
+                                               &xf);
+  else
+    update_r_body<T, false, false, false, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1,
+                                                nullptr, &xf);
 }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
@@ -3196,11 +3328,6 @@ __global__ __launch_bounds__(kBlock) void k_flush_defer(int64_t n, T *__restrict
   }
 }
 
-// Mode 4, slot 3 (after the body's update_r): the group's deferred x
-// updates, x = (((x + a0 p0) + a1 p1) + a2 p2) + a3 p3 over the slots that
-// ran in this group and no end-of-run flush applied (k_flush_defer's rule;
-// k_spmv_fd of the next slot 0 clears ran[]). 16-byte lanes; x and the p
-// buffers are not re-read before the next group overwrites them.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict__ x,
                                                         const T *__restrict__ P0,
@@ -3218,47 +3345,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict
     any = any || use[t];
   }
   if (!any) return;
-  using V = typename Vec2<T>::V;
-  const int64_t n2 = n >> 1;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  V *x2 = reinterpret_cast<V *>(x);
-  const V *Q[4] = {reinterpret_cast<const V *>(P0), reinterpret_cast<const V *>(P1),
-                   reinterpret_cast<const V *>(P2), reinterpret_cast<const V *>(P3)};
-  auto body = [&](int64_t i, auto sntc) {
-    constexpr bool S = decltype(sntc)::value;
-    V xv = ldv<S, T>(x2 + i);
-    V q[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) q[t] = ldv<S, T>(Q[t] + i);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (use[t]) {
-        xv.x = xv.x + a[t] * q[t].x;
-        xv.y = xv.y + a[t] * q[t].y;
-      }
-    }
-    stv<S, T>(x2 + i, xv);
-  };
-  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };
-  auto loop = [&](auto sntc) {
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + stride < n2; i += 2 * stride) {
-      body(E(i), sntc);
-      body(E(i + stride), sntc);
-    }
-    for (; i < n2; i += stride) body(E(i), sntc);
-  };
-  if (stream_nt<T>(n))
-    loop(std::true_type{});
-  else
-    loop(std::false_type{});
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    T xv = x[n - 1];
-    const T *Ps[4] = {P0, P1, P2, P3};
-    for (int t = 0; t < 4; ++t)
-      if (use[t]) xv = xv + a[t] * Ps[t][n - 1];
-    x[n - 1] = xv;
-  }
+  flush_group_range<T>(n, x, P0, P1, P2, P3, a, use, rev);
 }
 
 // *dst = sum of part[0..np) in sum_parts order (partitioned runs: the local
@@ -3409,8 +3496,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   X(133) X(135)                                                                             \
   X(267) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578)  \
   X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
-  X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122) X(40978)     \
-  X(106498) X(172034) X(303122) X(827410) X(9216000) X(9216002) X(10264576) X(10264578)     \
+  X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122)              \
+  X(9216000) X(9216002) X(10264576) X(10264578)                                             \
   X(12361728) X(12361730) X(20750336) X(20750338) X(29138944) X(29138946)
 template <typename T> const void *spmv_dot_kernel(int v) {
   switch (v) {
@@ -3492,14 +3579,40 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
                                int slot, RedWs<T> *ws, hipStream_t s, int rev) {
   CsrArgs a = args(A);
   a.rev = rev;
-  if (vl_active(A)) {  // the lean stencil walk: its own grid (the class layout's)
+  if (vl_whole(A)) {  // the lean stencil walk: its own grid (the class layout's)
     hipLaunchKernelGGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
                        ws);
     return hipGetLastError();
   }
+  if (A.sell_partial && (spmv_variant<T>(A) & (2048 | 8192))) {
+    // the SELL copy lacks the boundary rows: the whole matrix as CSR-stream
+    CsrDev d = A;
+    d.variant = 13;
+    d.lean = false;
+    d.rbo = nullptr;
+    return spmv_dot(d, p, Ap, st, slot, ws, s, rev);
+  }
   const int v = spmv_variant<T>(A);
   const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), v);
   CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
+}
+template <typename T>
+hipError_t Launch<T>::spmv_lean_interior(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,
+                                         int slot, RedWs<T> *ws, hipStream_t s, int rev,
+                                         const PeerDev *P, int wg0) {
+  if (!vl_active(A) || !A.vl_split || (P && (wg0 < 0 || wg0 % 8))) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  a.part_off = 0;
+  a.wg0 = P ? wg0 : 0;
+  if (P) {
+    hipLaunchKernelGGL(k_spmv_lean_push<T>, dim3(a.wg0 + A.vl_grid), dim3(kBlock), 0, s, a, p, Ap,
+                       st, slot, ws, *P);
+  } else {
+    hipLaunchKernelGGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
+                       ws);
+  }
+  return hipGetLastError();
 }
 // SpMV + p.Ap over a list of SELL slices (a partitioned matrix's interior or
 // boundary slices), its partials at [part_off, part_off + grid)
@@ -3534,23 +3647,10 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
   }
   const int vv = spmv_variant<T>(A, v);
   const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), vv);
-  switch (vv) {  // timing ablations (bits 16/32) exist for this kernel only
+  switch (vv) {  // CSR-stream timing ablations (bits 16 / 32), tuning only
     case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 63: CGX_LAUNCH_V(k_spmv_dot, 63, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 2064: CGX_LAUNCH_V(k_spmv_dot, 2064, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 2066: CGX_LAUNCH_V(k_spmv_dot, 2066, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 2072: CGX_LAUNCH_V(k_spmv_dot, 2072, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 2074: CGX_LAUNCH_V(k_spmv_dot, 2074, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 6160: CGX_LAUNCH_V(k_spmv_dot, 6160, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 6162: CGX_LAUNCH_V(k_spmv_dot, 6162, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 8210: CGX_LAUNCH_V(k_spmv_dot, 8210, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 40978: CGX_LAUNCH_V(k_spmv_dot, 40978, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 106498: CGX_LAUNCH_V(k_spmv_dot, 106498, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 172034: CGX_LAUNCH_V(k_spmv_dot, 172034, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 303122: CGX_LAUNCH_V(k_spmv_dot, 303122, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 827410: CGX_LAUNCH_V(k_spmv_dot, 827410, args(A), (const T *)A.val, p, Ap, st, 0, ws);
-    case 3973138: CGX_LAUNCH_V(k_spmv_dot, 3973138, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -3638,7 +3738,7 @@ template <typename T> bool Launch<T>::fd_supported(const CsrDev &A) {
 // to rounding (the sum order of one dot), not bit for bit. Holding k_spmv_fd
 // to k_spmv_dot's waves per SIMD instead spilled 20-56 VGPRs to scratch.
 template <typename T> int Launch<T>::fd_parts(const CsrDev &A) {
-  if (vl_active(A)) return A.vl_grid;
+  if (vl_whole(A)) return A.vl_grid;
   const int grid = grid_rows(A.nrb);
   const int r = spmv_fd_resident<T>(spmv_variant<T>(A));
   return (r > 0 && r < grid) ? r : grid;
@@ -3652,7 +3752,7 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   CsrArgs a = args(A);
   a.rev = rev;
   if constexpr (std::is_same<T, double>::value) {
-    if (vl_active(A)) {  // the lean walk at its class layout's grid
+    if (vl_whole(A)) {  // the lean walk at its class layout's grid
       hipLaunchKernelGGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
                          Ap, st, slot, ws, np_rr);
       return hipGetLastError();
@@ -3685,6 +3785,7 @@ template <typename T> static const void *spmv_bnd_kernel(int v) {
 #define CGX_KBN(VV) \
   case VV: return reinterpret_cast<const void *>(&k_spmv_dot_bnd<T, VV>);
     CGX_PUSH_LIST(CGX_KBN)
+    CGX_KBN(13) CGX_KBN(0)  // the boundary rows as CSR-stream blocks (spmv_dot_rows)
 #undef CGX_KBN
     default: return nullptr;
   }
@@ -3712,6 +3813,32 @@ hipError_t Launch<T>::spmv_dot_slices_bnd(const CsrDev &A, const int *list, int 
   return hipLaunchKernel(k, dim3(slice_grid(A, count)), dim3(kBlock), kargs, 0, s);
 }
 
+template <typename T> int Launch<T>::rows_grid(const CsrDev &A, int count) {
+  return cap_resident<T>(grid_rows(count), spmv_variant<T>(A, 13));
+}
+template <typename T>
+hipError_t Launch<T>::spmv_dot_rows(const CsrDev &A, const int *blocks, int count, int part_off,
+                                    const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
+                                    hipStream_t s, const PeerDev *P) {
+  const int v = spmv_variant<T>(A, 13);  // 13, or 0 for unaligned val / col
+  if (count < 1 || (v != 13 && v != 0)) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rbo = blocks;
+  a.nrb = count;
+  a.part_off = part_off;
+  const T *val = (const T *)A.val;
+  const int grid = rows_grid(A, count);
+  if (P) {
+    const void *k = spmv_bnd_kernel<T>(v);
+    PeerDev pd = *P;
+    void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
+                     (void *)&ws, (void *)&pd};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlock), kargs, 0, s);
+  }
+  const int spmv_grid_ = grid;
+  if (v == 13) CGX_LAUNCH_V(k_spmv_dot, 13, a, val, p, Ap, st, slot, ws);
+  CGX_LAUNCH_V(k_spmv_dot, 0, a, val, p, Ap, st, slot, ws);
+}
 template <typename T> bool Launch<T>::push_supported(const CsrDev &A) {
   return spmv_push_kernel<T>(spmv_variant<T>(A) & ~2097152) != nullptr;
 }
@@ -3752,11 +3879,21 @@ hipError_t Launch<T>::flush_group(int64_t n, T *x, T *const P[4], CgScalars<T> *
              (const T *)P[1], (const T *)P[2], (const T *)P[3], (const CgScalars<T> *)st, rev);
 }
 template <typename T>
+hipError_t Launch<T>::update_r_flush(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
+                                     RedWs<T> *ws, int np_pap, int rev, T *x, T *const P[4],
+                                     hipStream_t s) {
+  const XFlush<T> xf{x, {P[0], P[1], P[2], P[3]}};
+  CGX_LAUNCH(k_update_r_flush<T>, grid_elems(n, kGridUpdateR), n, r, Ap, st, slot, ws, np_pap,
+             rev, xf);
+}
+template <typename T>
 hipError_t Launch<T>::rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s) {
   CGX_LAUNCH(k_rr_settle<T>, 1, st, ws, np_rr);
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
-  if (vl_active(A)) return A.vl_grid;
+  if (vl_whole(A)) return A.vl_grid;
+  if (A.sell_partial && (spmv_variant<T>(A) & (2048 | 8192)))  // spmv_dot's CSR-stream
+    return cap_resident<T>(grid_rows(A.nrb), spmv_variant<T>(A, 13));
   return cap_resident<T>(grid_rows(A.nrb), spmv_variant<T>(A));  // = spmv_dot's grid
 }
 template <typename T> int Launch<T>::update_parts(int64_t n) {

@@ -167,11 +167,17 @@ struct cgx_csr {
   std::vector<int> sell_pool;               // the SELL-P pattern pool (host copy)
   std::vector<unsigned char> vl_slice_cls;  // class per slice (0xff: per-slice form)
   int vl_ncls = 0;
+  std::vector<cgx::VlClass> vl_tab_h;  // the class table (host copy, for a re-layout)
   void *d_vl_cls = nullptr, *d_vl_tab = nullptr;
   // partitioned SELL matrix: slices without ghost columns, then those with
   // (d_split[0, split_ni) interior, [split_ni, split_ni + split_nb) boundary)
   int *d_split = nullptr;
   int split_ni = 0, split_nb = 0;
+  // the boundary rows as CSR-stream row blocks (block ids into dev.rb; the
+  // schedule is cut at the boundary runs' ends): the boundary launch runs
+  // CSR-stream, in the rows' own entry order
+  int *d_bnd_blk = nullptr;
+  int bnd_nblk = 0;
   bool split_ordered = false;  // interior list in the chunked visit order
   hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
   cgx::Peer peer;  // device peer transport (cgx_dist_peer_enable)

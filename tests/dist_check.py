@@ -94,6 +94,13 @@ def main():
     check(L.cgx_csr_halo_info(A, C.byref(ghosts), C.byref(nbrs)))
     ni, nb = C.c_int(), C.c_int()
     check(L.cgx_csr_split_info(A, C.byref(ni), C.byref(nb)))
+    # the loop SpMV's form: the lean walk over the interior slices (variant
+    # bit 33554432) or the slice-list form
+    var = C.c_int()
+    check(L.cgx_csr_variant(A, C.byref(var)))
+    lc, ls, lg, ld, la, lp = C.c_int(), C.c_int64(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(L.cgx_csr_lean_info(A, C.byref(lc), C.byref(ls), C.byref(lg), C.byref(ld), C.byref(la),
+                              C.byref(lp)))
     b = cga.DeviceArray(q, nl, np.float64)
     x = cga.DeviceArray(q, nl, np.float64)
     check(L.cgx_iota(q.handle, F64, b.ptr, nl, float(begin)))
@@ -110,7 +117,8 @@ def main():
     check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
     parts = [None] * world
     dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value),
-                                   int(peer.value), int(acalls.value)))
+                                   int(peer.value), int(acalls.value),
+                                   (int(var.value), int(ls.value))))
     # x to rank 0 as tensors, padded to the largest block (gloo gathers
     # equal sizes; blocks differ by at most one row)
     mx = max(counts)
@@ -142,6 +150,7 @@ def main():
                           "neighbours": [p[1] for p in parts],
                           "split": [p[2] for p in parts], "peer": [p[3] for p in parts],
                           "async_exchanges": [p[4] for p in parts],
+                          "variant_lean_slices": [p[5] for p in parts],
                           "x_sha": hashlib.sha256(xg.tobytes()).hexdigest()[:16],
                           "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)

@@ -84,6 +84,40 @@ def test_async_host_halo_matches_synchronous(nproc, grid, mode):
     assert ra["x_sha"] == rs["x_sha"]
 
 
+@pytest.mark.parametrize("nproc,transport", [(2, "host-peer"), (2, "host"), (3, "host-peer")])
+def test_partitioned_lean_interior(nproc, transport):
+    """Every rank's slab gets the SELL-P value-code layout and the lean walk
+    (DESIGN.md §9): the boundary rows (ghost columns; from a lower rank they
+    are numbered after the own rows, so those rows are unsorted locally) are
+    placeholders in the SELL copy and run as CSR-stream blocks in the
+    boundary launch; the lean layout skips their slices (class 0xfe) and the
+    interior launch walks the rest (with the halo push in its first
+    workgroups on the peer transport). 128 x 128 x 48 over 2 and 3 ranks,
+    the walk forced at creation; x against the oracle (rel 1e-10)."""
+    r = _run(nproc, transport, 48, 3, ["--nxy", "128", "--bodies", "30"],
+             env={"CGX_SPMV_VARIANT": "33554432:0"})
+    assert r["ok"], r
+    assert r["bodies"] == 30
+    planes = 48 // nproc
+    for var, lean_slices in r["variant_lean_slices"]:
+        assert var & 33554432, r["variant_lean_slices"]
+        # nearly every slice of the slab but its boundary plane(s) is lean
+        # (a few interior slices keep the per-slice form)
+        assert lean_slices >= (planes - 3) * 128, r["variant_lean_slices"]
+    assert all(ni > 0 and nb > 0 for ni, nb in r["split"]), r["split"]
+
+
+def test_partitioned_ranks_share_the_sellp_layout():
+    """Without forcing a form, the ranks above rank 0 (whose boundary rows
+    gather ghosts numbered after their own rows) get the SELL-P value-code
+    layout as rank 0 does, not the dictionary SELL fallback of an unsorted
+    matrix (round 4 finding)."""
+    r = _run(3, "host", 48, 3, ["--nxy", "128", "--bodies", "20"])
+    assert r["ok"], r
+    fams = {var & (2048 | 4096 | 8192 | 32768) for var, _ in r["variant_lean_slices"]}
+    assert fams == {8192 | 32768}, r["variant_lean_slices"]
+
+
 def test_partitioned_slab_of_the_8gpu_config():
     """BASELINE config 4's per-rank shape: 512^3 over 8 GPUs gives each rank a
     512 x 512 x 64 slab and 2 MiB halo planes. Two such slabs (global

@@ -261,3 +261,40 @@ def test_sellp_rejects(oracle):
     rp = np.array([0, 2, 3], np.int32)
     cl = np.array([1, 0, 1], np.int32)
     assert sellp_plan(rp, cl) is None
+
+
+def test_sellp_refuses_the_upper_ranks_remapped_slab(oracle):
+    """Why a partitioned matrix's boundary slices are placeholders in its SELL
+    copy (cgx_dist.cpp): a rank's local numbering puts its own
+    rows first and its ghosts after them, so a row of rank 1 that gathers
+    from the plane below lists that ghost (local n_local + k) first in its
+    CSR order. The plain SELL-P plan refuses such a slab (its slots sum in
+    ascending local offset order); rank 0's slab, whose ghosts lie above,
+    and every row of rank 1 but its first plane's is sorted."""
+    from conjugategradient_amd._native import check, lib
+    L = lib()
+    nx, nz = 128, 8
+    rp, cl, _ = oracle.poisson(3, nx, nx, nz)
+    n = len(rp) - 1
+    nl = n // 2
+    plane = nx * nx
+    plans = []
+    for rank in (0, 1):
+        b = rank * nl
+        r = (rp[b:b + nl + 1] - rp[b]).astype(np.int32)
+        c = cl[rp[b]:rp[b + nl]].astype(np.int32).copy()
+        begins = (C.c_int64 * 2)(0, nl)
+        counts = (C.c_int64 * 2)(nl, nl)
+        ng, gh, rc = C.c_int64(), C.POINTER(C.c_int64)(), (C.c_int64 * 2)()
+        check(L.cgx_plan_ghosts(nl, b, len(c), c.ctypes.data, 2, begins, counts, C.byref(ng),
+                                C.byref(gh), rc))
+        assert ng.value == plane
+        check(L.cgx_plan_remap(nl, b, len(c), c.ctypes.data, ng.value, gh))
+        L.cgx_free_host(gh)
+        plans.append((r, c))
+    (r0, c0), (r1, c1) = plans
+    assert sellp_plan(r0, c0) is not None
+    assert sellp_plan(r1, c1) is None
+    # exactly its first plane's rows are the unsorted ones
+    unsorted = [i for i in range(nl) if (np.diff(c1[r1[i]:r1[i + 1]]) <= 0).any()]
+    assert unsorted == list(range(plane))
