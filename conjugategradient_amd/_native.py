@@ -92,6 +92,7 @@ _SIGS = {
     "cgx_cg_rxr": (_i32, [_vp, C.POINTER(_dbl)]),
     "cgx_cg_set_kernel_timing": (_i32, [_vp, _i32]),
     "cgx_cg_kernel_times": (_i32, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
+    "cgx_cg_kernel_exec_times": (_i32, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "cgx_cg_config": (_i32, [_vp, _i32, _i32]),
     "cgx_cg_set_mode": (_i32, [_vp, _i32]),
     "cgx_cg_coop_shape": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),

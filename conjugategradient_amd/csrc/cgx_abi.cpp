@@ -118,19 +118,26 @@ hipEvent_t next_event(cgx_cg *cg) {
   return cg->ev_pool[cg->ev_used++];
 }
 
-// Time one launch: records an event pair around `launch` when timing is on.
+// Time one launch when timing is on: an event pair around `launch` (the
+// launch as the stream sees it, dispatch latency included) and a pair its
+// first kernel's dispatch records itself (g_exec: the kernel's execution, as
+// rocprofv3 reports it; absent for launches that do not take them).
 template <class F> int timed(cgx_cg *cg, int kid, hipStream_t s, F &&launch) {
   if (!cg->timing) {
     CGX_HIP(launch());
     return CGX_OK;
   }
   const size_t i0 = cg->ev_used;
-  hipEvent_t e0 = next_event(cg), e1 = next_event(cg);
-  CGX_REQUIRE(e0 && e1, CGX_EHIP, "hipEventCreate failed");
+  hipEvent_t e0 = next_event(cg), e1 = next_event(cg), x0 = next_event(cg), x1 = next_event(cg);
+  CGX_REQUIRE(e0 && e1 && x0 && x1, CGX_EHIP, "hipEventCreate failed");
   CGX_HIP(hipEventRecord(e0, s));
-  CGX_HIP(launch());
+  g_exec = ExecTiming{x0, x1, false};
+  const hipError_t le = launch();
+  const bool used = g_exec.used;
+  g_exec = ExecTiming{};
+  CGX_HIP(le);
   CGX_HIP(hipEventRecord(e1, s));
-  cg->ev_pending.emplace_back(kid, i0);
+  cg->ev_pending.emplace_back(used ? kid + 16 : kid, i0);
   return CGX_OK;
 }
 
@@ -141,13 +148,20 @@ int harvest_events(cgx_cg *cg, int64_t active_iters) {
   int64_t iter_seen = 0;
   const int last_kid = cg->coop ? 1 : (cg->fused || cg->fdefer) ? 2 : 3;
   for (auto &pr : cg->ev_pending) {
-    const int kid = pr.first;
-    float ms = 0;
+    const bool exec = pr.first >= 16;  // the dispatch recorded its own pair too
+    const int kid = pr.first & 15;
+    float ms = 0, xs = 0;
     CGX_HIP(hipEventElapsedTime(&ms, cg->ev_pool[pr.second], cg->ev_pool[pr.second + 1]));
+    if (exec)
+      CGX_HIP(hipEventElapsedTime(&xs, cg->ev_pool[pr.second + 2], cg->ev_pool[pr.second + 3]));
     const bool count = kid == 0 || iter_seen < active_iters;
     if (count) {
       cg->t_ms[kid] += ms;
       cg->t_calls[kid] += 1;
+      if (exec) {
+        cg->t_exec_ms[kid] += xs;
+        cg->t_exec_calls[kid] += 1;
+      }
     }
     if (kid == last_kid) ++iter_seen;
   }
@@ -3032,9 +3046,27 @@ extern "C" int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable) {
   for (int i = 0; i < 4; ++i) {
     cg->t_ms[i] = 0;
     cg->t_calls[i] = 0;
+    cg->t_exec_ms[i] = 0;
+    cg->t_exec_calls[i] = 0;
   }
   cg->ev_pending.clear();
   cg->ev_used = 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_cg_kernel_exec_times(cgx_cg *cg, double *avg_ms, int64_t *calls) {
+  CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
+  DeviceGuard g(cg->ctx->device);
+  if (!cg->ev_pending.empty()) {
+    CGX_HIP(hipStreamSynchronize(cg->ctx->stream));
+    int rc = harvest_events(cg, 0);
+    if (rc) return rc;
+  }
+  for (int i = 0; i < 4; ++i) {
+    if (avg_ms)
+      avg_ms[i] = cg->t_exec_calls[i] ? cg->t_exec_ms[i] / (double)cg->t_exec_calls[i] : 0.0;
+    if (calls) calls[i] = cg->t_exec_calls[i];
+  }
   return CGX_OK;
 }
 

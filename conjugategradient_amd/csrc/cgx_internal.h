@@ -225,6 +225,17 @@ __host__ __device__ inline bool vl_whole(const CsrDev &A) {
   return vl_active(A) && !A.vl_split && !A.sell_partial;
 }
 
+// Kernel-execution timing (cgx_abi.cpp timed(), kernel timing on): the next
+// launch takes these start / stop events, recorded by its dispatch itself
+// (hipExtLaunchKernel: the kernel's own duration, as rocprofv3 reports it,
+// without the dispatch latency an event pair around the launch includes).
+// One launch consumes them; `used` tells the caller it happened.
+struct ExecTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool used = false;
+};
+extern thread_local ExecTiming g_exec;
+
 template <typename T> struct Launch {
   static int grid_rows(int nrb);
   static int grid_elems(int64_t n, int cap);

@@ -28,6 +28,7 @@
 //  * Build with -ffp-contract=off: every product is rounded before the add,
 //    as in the reference's expressions.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <map>
@@ -41,7 +42,31 @@
 #include "cgx_peer_dev.h"
 
 namespace cgx {
+thread_local ExecTiming g_exec;
 namespace {
+
+// a launch that takes the pending execution-timing events (g_exec) when set
+#define CGX_GGL(K, G, B, SH, S, ...)                                       \
+  do {                                                                    \
+    if (g_exec.start) {                                                   \
+      hipEvent_t e0_ = g_exec.start, e1_ = g_exec.stop;                   \
+      g_exec.start = g_exec.stop = nullptr;                               \
+      g_exec.used = true;                                                 \
+      hipExtLaunchKernelGGL(K, G, B, SH, S, e0_, e1_, 0, __VA_ARGS__);    \
+    } else {                                                              \
+      hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                    \
+    }                                                                     \
+  } while (0)
+inline hipError_t cgx_lk(const void *k, dim3 g, dim3 b, void **args, size_t sh, hipStream_t s) {
+  if (g_exec.start) {
+    hipEvent_t e0 = g_exec.start, e1 = g_exec.stop;
+    g_exec.start = g_exec.stop = nullptr;
+    g_exec.used = true;
+    return hipExtLaunchKernel(k, g, b, args, sh, s, e0, e1, 0);
+  }
+  return hipLaunchKernel(k, g, b, args, sh, s);
+}
+
 
 // ---------------------------------------------------------------------------
 // write-through (sc1) scalar hand-off helpers
@@ -3364,7 +3389,7 @@ template <typename T> __global__ void k_mark_defer(CgScalars<T> *st) {
 
 #define CGX_LAUNCH(kernel, grid, ...)                                              \
   do {                                                                             \
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, s, __VA_ARGS__);       \
+    CGX_GGL(kernel, dim3(grid), dim3(kBlock), 0, s, __VA_ARGS__);       \
     return hipGetLastError();                                                      \
   } while (0)
 
@@ -3412,7 +3437,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 
 #define CGX_LAUNCH_V(KERNEL, VV, ...)                                          \
   do {                                                                         \
-    hipLaunchKernelGGL((KERNEL<T, VV>), dim3(spmv_grid_), dim3(kBlock), 0, s,   \
+    CGX_GGL((KERNEL<T, VV>), dim3(spmv_grid_), dim3(kBlock), 0, s,   \
                        __VA_ARGS__);                                           \
     return hipGetLastError();                                                  \
   } while (0)
@@ -3580,7 +3605,7 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
   CsrArgs a = args(A);
   a.rev = rev;
   if (vl_whole(A)) {  // the lean stencil walk: its own grid (the class layout's)
-    hipLaunchKernelGGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
+    CGX_GGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
                        ws);
     return hipGetLastError();
   }
@@ -3606,10 +3631,10 @@ hipError_t Launch<T>::spmv_lean_interior(const CsrDev &A, const T *p, T *Ap, CgS
   a.part_off = 0;
   a.wg0 = P ? wg0 : 0;
   if (P) {
-    hipLaunchKernelGGL(k_spmv_lean_push<T>, dim3(a.wg0 + A.vl_grid), dim3(kBlock), 0, s, a, p, Ap,
+    CGX_GGL(k_spmv_lean_push<T>, dim3(a.wg0 + A.vl_grid), dim3(kBlock), 0, s, a, p, Ap,
                        st, slot, ws, *P);
   } else {
-    hipLaunchKernelGGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
+    CGX_GGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
                        ws);
   }
   return hipGetLastError();
@@ -3662,16 +3687,16 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
   if (!rin) rin = r;
   if (peer) {
     if (fused || rule || rin != r) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_update_r_peer<T>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
+    CGX_GGL((k_update_r_peer<T>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
                        s, n, r, Ap, st, slot, ws, np_pap, rev, *peer);
     return hipGetLastError();
   }
   if (fused) {
-    hipLaunchKernelGGL((k_update_r<T, true>), dim3(grid_elems(n, kMaxGrid)), dim3(kBlock), 0, s,
+    CGX_GGL((k_update_r<T, true>), dim3(grid_elems(n, kMaxGrid)), dim3(kBlock), 0, s,
                        n, rin, r,
                        Ap, st, slot, ws, 0, 0, 0);
   } else {
-    hipLaunchKernelGGL((k_update_r<T, false>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
+    CGX_GGL((k_update_r<T, false>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
                        s, n, rin, r, Ap, st, slot, ws, np_pap, rev, rule);
   }
   return hipGetLastError();
@@ -3753,7 +3778,7 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   a.rev = rev;
   if constexpr (std::is_same<T, double>::value) {
     if (vl_whole(A)) {  // the lean walk at its class layout's grid
-      hipLaunchKernelGGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
+      CGX_GGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
                          Ap, st, slot, ws, np_rr);
       return hipGetLastError();
     }
@@ -3761,7 +3786,7 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   const T *val = (const T *)A.val;
   void *kargs[] = {&a, (void *)&val, (void *)&r, (void *)&pold, (void *)&pc, (void *)&Ap,
                    (void *)&st, (void *)&slot, (void *)&ws, (void *)&np_rr};
-  return hipLaunchKernel(k, dim3(fd_parts(A)), dim3(kBlock), kargs, 0, s);
+  return cgx_lk(k, dim3(fd_parts(A)), dim3(kBlock), kargs, 0, s);
 }
 // ---- the interior SpMV with the halo push in front (k_spmv_dot_push): the
 // SELL forms a partitioned matrix takes (no plane march: slice lists)
@@ -3810,7 +3835,7 @@ hipError_t Launch<T>::spmv_dot_slices_bnd(const CsrDev &A, const int *list, int 
   PeerDev pd = P;
   void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
                    (void *)&ws, (void *)&pd};
-  return hipLaunchKernel(k, dim3(slice_grid(A, count)), dim3(kBlock), kargs, 0, s);
+  return cgx_lk(k, dim3(slice_grid(A, count)), dim3(kBlock), kargs, 0, s);
 }
 
 template <typename T> int Launch<T>::rows_grid(const CsrDev &A, int count) {
@@ -3833,7 +3858,7 @@ hipError_t Launch<T>::spmv_dot_rows(const CsrDev &A, const int *blocks, int coun
     PeerDev pd = *P;
     void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
                      (void *)&ws, (void *)&pd};
-    return hipLaunchKernel(k, dim3(grid), dim3(kBlock), kargs, 0, s);
+    return cgx_lk(k, dim3(grid), dim3(kBlock), kargs, 0, s);
   }
   const int spmv_grid_ = grid;
   if (v == 13) CGX_LAUNCH_V(k_spmv_dot, 13, a, val, p, Ap, st, slot, ws);
@@ -3868,7 +3893,7 @@ hipError_t Launch<T>::spmv_dot_slices_push(const CsrDev &A, const int *list, int
   PeerDev pd = P;
   void *kargs[] = {&a, (void *)&val, (void *)&p, (void *)&Ap, (void *)&st, (void *)&slot,
                    (void *)&ws, (void *)&pd};
-  return hipLaunchKernel(k, dim3(wg0 + slice_grid_push(A, count, wg0)), dim3(kBlock), kargs, 0,
+  return cgx_lk(k, dim3(wg0 + slice_grid_push(A, count, wg0)), dim3(kBlock), kargs, 0,
                          s);
 }
 
@@ -3963,12 +3988,12 @@ hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *cons
 template <typename T>
 hipError_t Launch<T>::flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                   hipStream_t s) {
-  hipLaunchKernelGGL(k_flush_defer<T>, dim3(elem_grid(n, 4)), dim3(kBlock), 0, s, n, x,
+  CGX_GGL(k_flush_defer<T>, dim3(elem_grid(n, 4)), dim3(kBlock), 0, s, n, x,
                      (const T *)P[0], (const T *)P[1], (const T *)P[2], (const T *)P[3],
                      (const CgScalars<T> *)st);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_mark_defer<T>, dim3(1), dim3(1), 0, s, st);
+  CGX_GGL(k_mark_defer<T>, dim3(1), dim3(1), 0, s, st);
   return hipGetLastError();
 }
 template <typename T>
@@ -3983,7 +4008,7 @@ hipError_t Launch<T>::axpby(int mode, int64_t n, const T *x, const T *y, const T
 }
 template <typename T>
 hipError_t Launch<T>::scalar_div(const T *num, const T *den, T *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_scalar_div<T>, dim3(1), dim3(1), 0, s, num, den, out);
+  CGX_GGL(k_scalar_div<T>, dim3(1), dim3(1), 0, s, num, den, out);
   return hipGetLastError();
 }
 template <typename T> hipError_t Launch<T>::fill(T *d, T v, int64_t n, hipStream_t s) {
@@ -4035,10 +4060,10 @@ hipError_t Launch<T>::sellp_pack(const CsrDev &A, const T *val, T *sval, void *m
                                  hipStream_t s) {
   const int g = elem_grid(A.nsl * kSellRows * 2, 4);
   if (A.sell_kind == 2)
-    hipLaunchKernelGGL((k_sellp_pack<T, unsigned>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
+    CGX_GGL((k_sellp_pack<T, unsigned>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
                        A.rowptr, A.col, val, A.sl, A.sdict, sval, (unsigned *)mask);
   else
-    hipLaunchKernelGGL((k_sellp_pack<T, unsigned char>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
+    CGX_GGL((k_sellp_pack<T, unsigned char>), dim3(g), dim3(kBlock), 0, s, A.n, A.nsl,
                        A.rowptr, A.col, val, A.sl, A.sdict, sval, (unsigned char *)mask);
   return hipGetLastError();
 }
@@ -4047,7 +4072,7 @@ template <typename T>
 hipError_t Launch<T>::sellpv_pack(const CsrDev &A, const T *val, const T *dict, int nd,
                                   unsigned char *codes, int *miss, T *missv, hipStream_t s) {
   const int g = elem_grid(A.nsl * kSellRows * 2, 4);
-  hipLaunchKernelGGL(k_sellpv_pack<T>, dim3(g), dim3(kBlock), 0, s, A.n, A.nsl, A.rowptr, A.col,
+  CGX_GGL(k_sellpv_pack<T>, dim3(g), dim3(kBlock), 0, s, A.n, A.nsl, A.rowptr, A.col,
                      val, A.sl, A.sdict, dict, nd, codes, miss, missv);
   return hipGetLastError();
 }
@@ -4055,21 +4080,21 @@ hipError_t Launch<T>::sellpv_pack(const CsrDev &A, const T *val, const T *dict, 
 template <typename T>
 hipError_t Launch<T>::vc_narrow(const void *codes8, void *codes4, int64_t chunks,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(k_vc_narrow, dim3(elem_grid(chunks, 4)), dim3(kBlock), 0, s,
+  CGX_GGL(k_vc_narrow, dim3(elem_grid(chunks, 4)), dim3(kBlock), 0, s,
                      (const unsigned char *)codes8, (unsigned char *)codes4, chunks);
   return hipGetLastError();
 }
 
 hipError_t vc_hash(const CsrDev &A, unsigned long long *hash, hipStream_t s) {
   const int g = (int)((A.nsl + 3) / 4);
-  hipLaunchKernelGGL(k_vc_hash, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
+  CGX_GGL(k_vc_hash, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
                      (const unsigned long long *)A.svc4, hash);
   return hipGetLastError();
 }
 hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, SellSlice *sl_t,
                     unsigned *count, hipStream_t s) {
   const int g = (int)((A.nsl + 3) / 4);
-  hipLaunchKernelGGL(k_vc_match, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
+  CGX_GGL(k_vc_match, dim3(g), dim3(kBlock), 0, s, A.sl, A.nsl,
                      (const unsigned long long *)A.svc4, tmpl, nt, sl_t, count);
   return hipGetLastError();
 }
@@ -4097,7 +4122,7 @@ hipError_t col16_build(const CsrDev &A, short *col16, unsigned *bad, hipStream_t
   hipError_t e = hipMemsetAsync(col16, 0, (size_t)(A.nnz + 2) * sizeof(short), s);
   if (e != hipSuccess) return e;
   const int grid = A.nrb < kMaxGrid ? A.nrb : kMaxGrid;
-  hipLaunchKernelGGL(k_col16, dim3(grid), dim3(kBlock), 0, s, A.rb, A.rbk, A.col, A.nrb, col16,
+  CGX_GGL(k_col16, dim3(grid), dim3(kBlock), 0, s, A.rb, A.rbk, A.col, A.nrb, col16,
                      bad);
   return hipGetLastError();
 }

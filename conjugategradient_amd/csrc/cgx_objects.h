@@ -227,6 +227,8 @@ struct cgx_cg {
   std::vector<std::pair<int, size_t>> ev_pending;  // (kernel id, event index)
   double t_ms[4] = {0, 0, 0, 0};
   int64_t t_calls[4] = {0, 0, 0, 0};
+  double t_exec_ms[4] = {0, 0, 0, 0};      // the dispatch's own event pairs (g_exec)
+  int64_t t_exec_calls[4] = {0, 0, 0, 0};
 };
 
 namespace cgx {

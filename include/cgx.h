@@ -200,6 +200,11 @@ int cgx_cg_rxr(cgx_cg *cg, double *rxr);
  * calls[0..3] = launches timed. */
 int cgx_cg_set_kernel_timing(cgx_cg *cg, int enable);
 int cgx_cg_kernel_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
+/* The same kernels' execution times: event pairs each kernel's dispatch
+ * records itself (hipExtLaunchKernel), so without the dispatch latency the
+ * pairs of cgx_cg_kernel_times include; the durations rocprofv3 reports.
+ * calls[i] = 0 where a launch did not record them. */
+int cgx_cg_kernel_exec_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
 /* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
 int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
 /* Iteration structure (before cgx_cg_begin): 0 auto (4 for the 2-D plane
