@@ -58,13 +58,14 @@ def main():
         check(L.cgx_cg_run(cg, steps, C.byref(tot), C.byref(st)))
         check(L.cgx_sync(q.handle))
         dt = time.perf_counter() - t
-        # per-kernel HIP-event pass (eager launches; the durations, not the gaps)
+        # per-kernel HIP-event pass (eager launches)
         avg = (C.c_double * 4)()
         calls = (C.c_int64 * 4)()
         check(L.cgx_cg_set_kernel_timing(cg, 1))
         check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, 101))
         check(L.cgx_cg_run(cg, 100, C.byref(tot), C.byref(st)))
-        check(L.cgx_cg_kernel_times(cg, avg, calls))
+        # the kernels' own durations (events their dispatches record)
+        check(L.cgx_cg_kernel_exec_times(cg, avg, calls))
         print(json.dumps({"slab": [nx, ny, nz], "dim": dim, "rows": n, "mode": mode.value,
                           "spmv_variant": v.value, "bodies": steps,
                           "us_per_body": round(dt / steps * 1e6, 2),
