@@ -2576,7 +2576,12 @@ static bool fd_auto(const cgx_cg *cg) {
   const int v = launch_variant(A->dev, cg->dtype);
   const bool march2d = (v & 2097152) && A->dev.march_a == 0;
   const bool small = A->dev.nnz * (int64_t)(sizeof(double) + sizeof(int)) < (int64_t(64) << 20);
-  return march2d || (small && (v & 1048576));
+  // the lean walk with cache-resident vectors (<= 32 MB, stream_nt's bound):
+  // the 256 x 256 x 32 slab 29.5-29.8 us per body in mode 4 against
+  // 31.9-32.1 in mode 3; at 256^3 mode 3 wins (5,182-5,208 against
+  // 4,750-4,807 it/s; profiles/r04_dist_ab.log, r04b_slab.log)
+  const bool lean_cached = vl_whole(A->dev) && A->dev.n <= (int64_t(4) << 20);
+  return march2d || (small && (v & 1048576)) || lean_cached;
 }
 
 // Auto mode picks 5 (the persistent body) for small single-device f64
