@@ -108,7 +108,8 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every core this job may use)")
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=40.0,
+                    help="wall-clock budget of the CPU baseline's runs (SURVEY §8(d): 5 runs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the csr_general block (general-value formats)")
@@ -204,9 +205,13 @@ def job_cores() -> dict:
             "nproc": os.cpu_count(), "model": model}
 
 
-def cpu_baseline(workload: str, grid, threads: int, budget_s: float):
-    """The oracle's OpenMP restatement of the reference iteration on a sample
-    of the same workload (same matrix, same b), timed on host cores."""
+def cpu_baseline(workload: str, grid, threads: int, budget_s: float, iters: int = 500,
+                 warmup: int = 20, reps: int = 5):
+    """The oracle's OpenMP restatement of the reference iteration on the same
+    workload (same matrix, same b), timed on host cores to the SURVEY §8(d)
+    protocol: `iters` (500) timed bodies after `warmup` (20) untimed ones,
+    the median of `reps` (5) runs, or of as many runs as fit in `budget_s`
+    (at least one; the sample names the count)."""
     import numpy as np
     from oracle import oracle as O
 
@@ -226,25 +231,56 @@ def cpu_baseline(workload: str, grid, threads: int, budget_s: float):
         what = workload
     n, nnz = len(rp) - 1, len(vl)
     b = np.arange(1, n + 1, dtype=np.float64)
-    t1, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, 2, threads)  # probe (also warms the pool)
-    iters = max(1, min(5000, int(budget_s / max(t1 / 2, 1e-6))))  # ~budget_s of CPU work
-    t, _ = O.cg_fixed_iters_omp(rp, cl, vl, b, iters, threads)
-    its = iters / t
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < reps:
+        t, _ = O.cg_timed_omp(rp, cl, vl, b, warmup, iters, threads)
+        times.append(t)
+        spent = time.perf_counter() - t_start
+        if spent + spent / len(times) > budget_s:  # the next run would pass the budget
+            break
+    med = float(np.median(times))
+    its = iters / med
     return {
         "value": round(b_alg(n, nnz) * its / 1e9, 3),
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
         "iterations_per_s": round(its, 3),
+        "protocol": {"timed_iterations": iters, "warmup_iterations": warmup,
+                     "runs": len(times), "runs_asked": reps, "statistic": "median",
+                     "run_seconds": [round(x, 3) for x in times]},
         "host": {"cpu_model": info["model"], "nproc": info["nproc"],
                  "affinity_cores": info["affinity"], "cgroup_cpu_quota": info["cgroup_quota"],
                  "declared_cpu_share": info["declared_share"],
                  "omp_proc_bind": os.environ.get("OMP_PROC_BIND")},
-        "sample": f"{what}, {iters} iterations of the reference command "
-                  f"sequence (oracle/cg_oracle.c orc_cg_fixed_iters_omp, OpenMP, "
-                  f"{threads} threads), {its:.3f} it/s, {t:.2f} s; value priced at the "
-                  f"CSR bytes B_alg",
+        "sample": f"{what}: K = {iters} timed iterations of the reference command sequence "
+                  f"after {warmup} untimed warm-up iterations (oracle/cg_oracle.c "
+                  f"orc_cg_timed_omp, OpenMP, {threads} threads), median of {len(times)} "
+                  f"run(s) of {reps} asked within a {budget_s:.0f} s budget: {its:.3f} it/s; "
+                  f"value priced at the CSR bytes B_alg",
     }
+
+
+TUNE_KINDS = {0: "k_spmv_dot", 1: "k_spmv_dot (interior slices)", 2: "k_spmv_fd",
+              3: "lean walk", 4: "lean walk (interior slices)"}
+
+
+def autotune_record(L, A) -> dict | None:
+    """The SpMV autotune's timings of this matrix (cgx_csr_autotune_record):
+    every form it timed, how, and its median µs per launch."""
+    n = C.c_int(0)
+    if not hasattr(L, "cgx_csr_autotune_record"):  # (an older $CGX_LIB A/B build)
+        return None
+    L.cgx_csr_autotune_record(A, None, None, None, 0, C.byref(n))
+    if n.value == 0:
+        return None
+    v, k, us = (C.c_int * n.value)(), (C.c_int * n.value)(), (C.c_float * n.value)()
+    L.cgx_csr_autotune_record(A, v, k, us, n.value, C.byref(n))
+    return {"rule": "median of 5 interleaved rounds of 3 launches per form; a form displaces "
+                    "the more specialised one only when >= 3% faster",
+            "forms": [{"variant": int(v[i]), "how": TUNE_KINDS.get(k[i], str(k[i])),
+                       "us": round(float(us[i]), 2)} for i in range(n.value)]}
 
 
 def rccl_timing(L, q, args, wl, b, x, transport, its, elapsed, world, dist) -> dict:
@@ -272,8 +308,14 @@ def rccl_timing(L, q, args, wl, b, x, transport, its, elapsed, world, dist) -> d
     check(L.cgx_cg_create(q.handle, A2, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
     check(L.cgx_cg_set_mode(cg, args.mode))
-    x.fill(0.0)
-    check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, args.warmup + args.steps))
+    # its own x: the timed run's cg continues in the profile pass after this
+    # (modes 3 / 4 hold deferred x updates for its x)
+    import numpy as np
+
+    import conjugategradient_amd as cga
+    x2 = cga.DeviceArray(q, wl.n_local, np.float64)
+    x2.fill(0.0)
+    check(L.cgx_cg_begin(cg, b.ptr, x2.ptr, 0.0, args.warmup + args.steps))
     bodies, stopped = C.c_int64(0), C.c_int(0)
     if args.warmup:
         check(L.cgx_cg_run(cg, args.warmup, C.byref(bodies), C.byref(stopped)))
@@ -424,6 +466,7 @@ def run(args) -> None:
     lean = [C.c_int(0), C.c_int64(0), C.c_int(0), C.c_int(0), C.c_int(0), C.c_int(0)]
     check(L.cgx_csr_lean_info(A, *[C.byref(v) for v in lean]))
     lean_on = bool(variant.value & KVL)
+    autotune = autotune_record(L, A)
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
@@ -604,6 +647,7 @@ def run(args) -> None:
                                         "grid-wide exchanges per body)"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
                        "spmv_variant": int(variant.value),
+                       "spmv_autotune": autotune,
                        "value_code_templates": (
                            {"templates": ntpl.value, "slices": tpl_slices.value,
                             "slices_total": (n_local + 127) // 128,

@@ -1149,6 +1149,8 @@ void free_sell(cgx_csr *A) {
   A->dev.nvt = 0;
   A->vt_slices = 0;
   A->split_ni = A->split_nb = 0;
+  A->split_bd_h.clear();
+  A->split_ordered = false;
   if (A->d_bnd_blk) (void)hipFree(A->d_bnd_blk);
   A->d_bnd_blk = nullptr;
   A->bnd_nblk = 0;
@@ -1762,7 +1764,10 @@ static int build_lean_classes(cgx_csr *A, std::vector<VlClass> &tab) {
 // of 8: waves of XCD group g walk its eighth of the slices with step G / 2)
 // and the table, on the device; the lean walk is then available at grid G.
 static int build_lean_layout(cgx_csr *A, const std::vector<VlClass> &tab, int G) {
-  if (A->vl_slice_cls.empty() || tab.empty() || G < 8 || G % 8) return CGX_EINVAL;
+  // (G <= kMaxGrid: the walk's p.Ap partials land in RedWs::pap_part, and a
+  // split matrix's boundary launch writes its own after them)
+  if (A->vl_slice_cls.empty() || tab.empty() || G < 8 || G % 8 || G > kMaxGrid)
+    return CGX_EINVAL;
   const int64_t nsl = A->dev.nsl;
   const int step = G / 2;
   // the chunked walk (spmv_lean) where a plane holds several chunks of step
@@ -2094,6 +2099,19 @@ extern "C" int cgx_csr_lean_info(cgx_csr *A, int *classes, int64_t *slices, int 
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_autotune_record(cgx_csr *A, int *variants, int *kinds, float *us,
+                                       int cap, int *count) {
+  CGX_REQUIRE(A && count && cap >= 0, CGX_EINVAL, "bad argument");
+  CGX_REQUIRE(cap == 0 || (variants && kinds && us), CGX_EINVAL, "NULL output array");
+  *count = (int)A->tune.size();
+  for (int i = 0; i < cap && i < *count; ++i) {
+    variants[i] = A->tune[(size_t)i].variant;
+    kinds[i] = A->tune[(size_t)i].kind;
+    us[i] = A->tune[(size_t)i].us;
+  }
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_march_info(cgx_csr *A, int *stride, int *offset_a, int *run_planes) {
   CGX_REQUIRE(A && stride && offset_a && run_planes, CGX_EINVAL, "NULL argument");
   const bool on = A->dev.svc && A->dev.sell_maxw <= 8 && A->dev.march_k > 0;
@@ -2149,6 +2167,11 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
     }
     A->dev.variant = kVlBase;
     A->dev.lean = true;
+    // a split partitioned matrix: the walk runs its interior only (the
+    // boundary slices class 0xfe), as cgx_csr_create_dist leaves it
+    if (A->split_ni > 0 && !A->dev.vl_split) {
+      if (int rc = lean_mark_split(A, A->split_bd_h)) return rc;
+    }
     return CGX_OK;
   }
   A->dev.lean = false;
@@ -2188,7 +2211,50 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
 // streams 9 B per entry instead of 12) and is cheap to measure — a
 // few launches on scratch vectors. $CGX_SPMV_VARIANT forces a variant. The
 // SELL copy is freed when a CSR-stream variant wins.
+//
+// Every candidate is timed in kTuneRounds interleaved rounds (3 launches
+// each after one warm-up launch) and scored by its median round. The
+// candidates are ranked by preference (the most specialised form first: the
+// lean walk, then the value-code forms with templates ... down to plain
+// CSR-stream), and a candidate displaces the preferred one only when its
+// median is at least kTuneMargin faster: two forms within a few percent of
+// each other no longer flip with a box's momentary state (VERDICT r4:
+// 565250 in one rep, 10264578 in the next of the same command). The record
+// (every candidate's median µs per launch) is kept on the matrix
+// (cgx_csr_autotune_record).
+//
+// A partitioned matrix whose SELL copy is split (interior slices without
+// ghost columns, boundary slices with: cgx_dist.cpp) is timed on what its
+// loop runs there: the SELL forms over the interior slice list, the lean
+// walk over the interior slices (boundary slices class 0xfe).
+constexpr int kTuneRounds = 5;
+constexpr float kTuneMargin = 0.03f;
+
+static int tune_pick(const std::vector<float> &med) {  // med in preference order
+  int inc = 0;
+  for (int i = 1; i < (int)med.size(); ++i)
+    if (med[(size_t)i] < med[(size_t)inc] * (1.0f - kTuneMargin)) inc = i;
+  return inc;
+}
+
+static float median_of(std::vector<float> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 1e30f : v[v.size() / 2];
+}
+
+// the boundary slices of a split matrix marked 0xfe in its lean class list
+// and the layout rebuilt at grid G (lean_mark_split without the lean flag)
+static int lean_split_layout(cgx_csr *A, int G) {
+  for (int q : A->split_bd_h)
+    if (q >= 0 && (size_t)q < A->vl_slice_cls.size()) A->vl_slice_cls[(size_t)q] = 0xfe;
+  const std::vector<VlClass> tab = A->vl_tab_h;
+  if (int rc = build_lean_layout(A, tab, G)) return rc;
+  A->dev.vl_split = 1;
+  return CGX_OK;
+}
+
 int autotune_spmv(cgx_csr *A) {
+  A->tune.clear();
   if (const char *env = std::getenv("CGX_SPMV_VARIANT")) {
     // the same checks as cgx_csr_set_variant: a mistyped value fails here,
     // not later as a kernel launch error; "V:G" forces the lean walk's grid
@@ -2253,6 +2319,11 @@ int autotune_spmv(cgx_csr *A) {
       cands.push_back(2050 | 32768 | c4 | pipe);
     }
   }
+  // preference order: the most specialised form first (the list above grows
+  // in that direction)
+  std::reverse(cands.begin(), cands.end());
+  // a split partitioned matrix: the SELL forms time its interior slice list
+  const bool split = A->dist && A->d_split && A->split_ni > 0 && A->dev.sl;
   cgx_ctx *ctx = A->ctx;
   hipStream_t s = ctx->stream;
   const size_t es = dtype_size(A->dtype);
@@ -2270,87 +2341,111 @@ int autotune_spmv(cgx_csr *A) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
-  // interleaved rounds, best of each candidate: one round alone picks by
-  // the device's momentary state when candidates are within a few percent
-  std::vector<float> tbest(cands.size(), 1e30f);
-  for (int round = 0; round < 3 && e == hipSuccess; ++round) {
-    for (size_t ci = 0; ci < cands.size() && e == hipSuccess; ++ci) {
-      const int v = cands[ci];
-      // the candidate as the matrix's variant (the kernel arguments follow
-      // it: the kVT forms read the template slice table)
-      CsrDev dv = A->dev;
-      dv.variant = v;
-      float tot = 0;
-      for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
-        if (rep == 1) e = hipEventRecord(e0, s);
-        if (e != hipSuccess) break;
-        if (A->dtype == CGX_F32)
-          e = Launch<float>::spmv_dot_variant(v, dv, (const float *)x, (float *)y,
-                                              (CgScalars<float> *)st, (RedWs<float> *)ctx->ws,
-                                              s);
-        else
-          e = Launch<double>::spmv_dot_variant(v, dv, (const double *)x, (double *)y,
-                                               (CgScalars<double> *)st,
-                                               (RedWs<double> *)ctx->ws, s);
-      }
-      if (e == hipSuccess) e = hipEventRecord(e1, s);
-      if (e == hipSuccess) e = hipEventSynchronize(e1);
-      if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
-      if (e == hipSuccess) tbest[ci] = std::min(tbest[ci], tot);
-      if (e != hipSuccess) {
-        set_error("cgx_csr_create: SpMV autotune candidate %d (resolved %d) failed: %s", v,
-                  launch_variant(dv, A->dtype), hipGetErrorString(e));
-        for (void *p : {x, y, st})
-          if (p) (void)hipFree(p);
-        return CGX_EHIP;
-      }
+  // one launch of candidate form `how` (0: k_spmv_dot of dv's variant over
+  // the matrix or, split, its interior slices; 1: the lean walk (interior
+  // when split); 2: k_spmv_fd)
+  void *ap = nullptr;
+  bool err_set = false;
+  auto launch = [&](const CsrDev &dv, int how) -> hipError_t {
+    if (A->dtype == CGX_F32) {
+      CgScalars<float> *sf = (CgScalars<float> *)st;
+      RedWs<float> *wf = (RedWs<float> *)ctx->ws;
+      if (how == 1)
+        return split ? Launch<float>::spmv_lean_interior(dv, (const float *)x, (float *)y, sf, 0,
+                                                         wf, s, 0, nullptr, 0)
+                     : Launch<float>::spmv_dot(dv, (const float *)x, (float *)y, sf, 0, wf, s);
+      if (split && (dv.variant & (2048 | 8192)))
+        return Launch<float>::spmv_dot_slices(dv, A->d_split, A->split_ni, 0, (const float *)x,
+                                              (float *)y, sf, 0, wf, s);
+      return Launch<float>::spmv_dot_variant(dv.variant, dv, (const float *)x, (float *)y, sf,
+                                             wf, s);
     }
+    CgScalars<double> *sd = (CgScalars<double> *)st;
+    RedWs<double> *wd = (RedWs<double> *)ctx->ws;
+    if (how == 2)
+      return Launch<double>::spmv_fd(dv, (const double *)x, (const double *)x, (double *)y,
+                                     (double *)ap, sd, 0, wd, Launch<double>::update_parts(A->dev.n),
+                                     s);
+    if (how == 1)
+      return split ? Launch<double>::spmv_lean_interior(dv, (const double *)x, (double *)y, sd, 0,
+                                                        wd, s, 0, nullptr, 0)
+                   : Launch<double>::spmv_dot(dv, (const double *)x, (double *)y, sd, 0, wd, s);
+    if (split && (dv.variant & (2048 | 8192)))
+      return Launch<double>::spmv_dot_slices(dv, A->d_split, A->split_ni, 0, (const double *)x,
+                                             (double *)y, sd, 0, wd, s);
+    return Launch<double>::spmv_dot_variant(dv.variant, dv, (const double *)x, (double *)y, sd, wd,
+                                            s);
+  };
+  // interleaved rounds over the forms; per form the median round's µs per
+  // launch (3 launches after a warm-up one)
+  auto time_forms = [&](const std::vector<CsrDev> &forms, const std::vector<int> &how,
+                        std::vector<float> &med) {
+    std::vector<std::vector<float>> t(forms.size());
+    for (int round = 0; round < kTuneRounds && e == hipSuccess; ++round)
+      for (size_t ci = 0; ci < forms.size() && e == hipSuccess; ++ci) {
+        float tot = 0;
+        for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
+          if (rep == 1) e = hipEventRecord(e0, s);
+          if (e == hipSuccess) e = launch(forms[ci], how[ci]);
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, s);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
+        if (e == hipSuccess) t[ci].push_back(tot * 1e3f / 3);
+        if (e != hipSuccess && !err_set) {
+          set_error("cgx_csr_create: SpMV autotune candidate %d (resolved %d) failed: %s",
+                    forms[ci].variant, launch_variant(forms[ci], A->dtype), hipGetErrorString(e));
+          err_set = true;
+        }
+      }
+    med.resize(forms.size());
+    for (size_t ci = 0; ci < forms.size(); ++ci) med[ci] = median_of(t[ci]);
+  };
+  std::vector<CsrDev> forms;
+  std::vector<int> how;
+  for (int v : cands) {
+    CsrDev dv = A->dev;  // the candidate as the matrix's variant (kVT: template slice table)
+    dv.variant = v;
+    dv.lean = false;
+    forms.push_back(dv);
+    how.push_back(0);
   }
+  std::vector<float> med;
+  time_forms(forms, how, med);
   int best_v = 0;
-  float best = 1e30f;
-  for (size_t ci = 0; ci < cands.size(); ++ci)
-    if (tbest[ci] < best) {
-      best = tbest[ci];
-      best_v = cands[ci];
-    }
+  float best_us = 1e30f;
+  if (e == hipSuccess) {
+    const int k = tune_pick(med);
+    best_v = cands[(size_t)k];
+    best_us = med[(size_t)k];
+    for (size_t ci = 0; ci < cands.size(); ++ci)
+      A->tune.push_back({cands[ci], split ? 1 : 0, med[ci]});
+  }
   // A 2-D plane-march winner runs the loop as mode 4 (fd_auto), i.e. as
   // k_spmv_fd, whose register budget differs from k_spmv_dot's: with value-
   // code templates it holds 3 waves per SIMD against 2 (152 against 169
   // VGPRs) while k_spmv_dot loses one (profiles/r03_vt3.log: 4096^2 loop
   // 95-99 against 103-104 us, isolated k_spmv_dot 58.6 against 54.2). The
-  // march and its template form are therefore decided on their fd kernels.
-  if (e == hipSuccess && A->dtype == CGX_F64 && (best_v & 2097152) && !(best_v & kVT) &&
-      A->dev.march_k > 0 && A->dev.march_a == 0 && A->dev.sl_t) {
-    const int pair[2] = {best_v, best_v | kVT};
-    float tf[2] = {1e30f, 1e30f};
-    void *ap = nullptr;
+  // march and its template form are therefore decided on their fd kernels
+  // (the template form preferred).
+  if (e == hipSuccess && !split && A->dtype == CGX_F64 && (best_v & 2097152) &&
+      !(best_v & kVT) && A->dev.march_k > 0 && A->dev.march_a == 0 && A->dev.sl_t) {
     e = hipMalloc(&ap, nx * es);
-    const int npr = Launch<double>::update_parts(A->dev.n);
-    for (int round = 0; round < 3 && e == hipSuccess; ++round)
-      for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-        CsrDev dv = A->dev;
-        dv.variant = pair[k];
-        float tot = 0;
-        for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
-          if (rep == 1) e = hipEventRecord(e0, s);
-          if (e == hipSuccess)
-            e = Launch<double>::spmv_fd(dv, (const double *)x, (const double *)x, (double *)y,
-                                        (double *)ap, (CgScalars<double> *)st, 0,
-                                        (RedWs<double> *)ctx->ws, npr, s);
-        }
-        if (e == hipSuccess) e = hipEventRecord(e1, s);
-        if (e == hipSuccess) e = hipEventSynchronize(e1);
-        if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
-        if (e == hipSuccess) tf[k] = std::min(tf[k], tot);
-      }
-    if (ap) (void)hipFree(ap);
-    if (e == hipSuccess && tf[1] < tf[0]) best_v = pair[1];
+    std::vector<CsrDev> fdf(2, A->dev);
+    fdf[0].variant = best_v | kVT;
+    fdf[1].variant = best_v;
+    std::vector<float> fm;
+    if (e == hipSuccess) time_forms(fdf, {2, 2}, fm);
+    if (e == hipSuccess) {
+      for (int k = 0; k < 2; ++k) A->tune.push_back({fdf[(size_t)k].variant, 2, fm[(size_t)k]});
+      if (tune_pick(fm) == 0) best_v |= kVT;
+    }
   }
-  // The lean stencil walk (kVL) at its grid against the winner so far,
-  // interleaved rounds as above (its generic slices run the template
-  // value-code form, its base variant). (A software-pipelined form, two
-  // slices' gathers in flight per wave, measured slower in the loop: 747
-  // against 631 us at 512^3, profiles/r04_lean_pipe512.log; not built.)
+  // The lean stencil walk (kVL) at its grid against the winner so far, the
+  // walk preferred (its generic slices run the template value-code form, its
+  // base variant). (A software-pipelined form, two slices' gathers in flight
+  // per wave, measured slower in the loop: 747 against 631 us at 512^3,
+  // profiles/r04_lean_pipe512.log; not built.)
   std::vector<VlClass> vtab;
   int lean_G = 0;
   // A 2-D plane-march winner runs the loop in mode 4 (fd_auto: two kernels
@@ -2362,44 +2457,33 @@ int autotune_spmv(cgx_csr *A) {
       !vtab.empty()) {
     const int G = lean_grid(A);
     if (build_lean_layout(A, vtab, G) != CGX_OK) e = hipErrorOutOfMemory;
-    float tl[2] = {1e30f, 1e30f};  // the incumbent, the lean walk
-    for (int round = 0; round < 3 && e == hipSuccess; ++round)
-      for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-        CsrDev dv = A->dev;
-        dv.variant = k ? kVlBase : best_v;
-        dv.lean = k == 1;
-        float tot = 0;
-        for (int rep = 0; rep < 4 && e == hipSuccess; ++rep) {
-          if (rep == 1) e = hipEventRecord(e0, s);
-          if (e != hipSuccess) break;
-          if (A->dtype == CGX_F32)
-            e = k ? Launch<float>::spmv_dot(dv, (const float *)x, (float *)y,
-                                            (CgScalars<float> *)st, 0, (RedWs<float> *)ctx->ws, s)
-                  : Launch<float>::spmv_dot_variant(best_v, dv, (const float *)x, (float *)y,
-                                                    (CgScalars<float> *)st,
-                                                    (RedWs<float> *)ctx->ws, s);
-          else
-            e = k ? Launch<double>::spmv_dot(dv, (const double *)x, (double *)y,
-                                             (CgScalars<double> *)st, 0,
-                                             (RedWs<double> *)ctx->ws, s)
-                  : Launch<double>::spmv_dot_variant(best_v, dv, (const double *)x, (double *)y,
-                                                     (CgScalars<double> *)st,
-                                                     (RedWs<double> *)ctx->ws, s);
-        }
-        if (e == hipSuccess) e = hipEventRecord(e1, s);
-        if (e == hipSuccess) e = hipEventSynchronize(e1);
-        if (e == hipSuccess) e = hipEventElapsedTime(&tot, e0, e1);
-        if (e == hipSuccess) tl[k] = std::min(tl[k], tot);
-      }
-    if (e == hipSuccess && tl[1] < tl[0]) lean_G = G;
+    if (e == hipSuccess && split && lean_split_layout(A, G) != CGX_OK) e = hipErrorOutOfMemory;
+    std::vector<CsrDev> lf(2, A->dev);
+    lf[0].variant = kVlBase;
+    lf[0].lean = true;
+    lf[1].variant = best_v;
+    lf[1].lean = false;
+    std::vector<float> lm;
+    if (e == hipSuccess) time_forms(lf, {1, 0}, lm);
+    if (e == hipSuccess) {
+      A->tune.push_back({kVL | kVlBase, split ? 4 : 3, lm[0]});
+      if (tune_pick(lm) == 0) lean_G = G;
+      else best_us = lm[1];
+    }
   }
+  (void)best_us;
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
-  for (void *p : {x, y, st})
+  for (void *p : {x, y, st, ap})
     if (p) (void)hipFree(p);
-  if (e != hipSuccess) free_lean(A);
-  CGX_HIP(e);
+  if (e != hipSuccess) {
+    free_lean(A);
+    A->tune.clear();
+    if (!err_set) set_error("cgx_csr_create: SpMV autotune: %s", hipGetErrorString(e));
+    return CGX_EHIP;
+  }
   if (lean_G > 0) {
+    // (a split matrix keeps its boundary marks and vl_split)
     if (int rc = build_lean_layout(A, vtab, lean_G)) return rc;
     A->dev.variant = kVlBase;
     A->dev.lean = true;

@@ -628,14 +628,15 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   // the boundary slices are placeholders in the SELL copy (their rows may be
   // unsorted locally: ghosts from lower ranks are numbered after the own
   // rows); the boundary launch runs their rows as CSR-stream blocks
-  if ((rc = build_sell(A, hrp.data(), hcol.data(), 0, h.n_ghost > 0 ? &bslice : nullptr)) ||
-      (rc = autotune_spmv(A))) {
+  if ((rc = build_sell(A, hrp.data(), hcol.data(), 0, h.n_ghost > 0 ? &bslice : nullptr))) {
     cgx_csr_destroy(A);
     return rc;
   }
   // interior / boundary slices of the SELL copy: the halo exchange overlaps
   // the interior ones (enqueue_iter); a slab of a stencil has one boundary
-  // plane per neighbour
+  // plane per neighbour. Built before the autotune, which times the SELL
+  // forms and the lean walk over the interior list (freed with the SELL copy
+  // when a CSR-stream form wins).
   if (A->dev.sl && h.n_ghost > 0) {
     const int64_t H = (int64_t)kSellRows * A->dev.sell_r, nsl = A->dev.nsl;
     std::vector<int> in, bd;
@@ -663,14 +664,17 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
       }
     }
     if (!in.empty() && !bd.empty()) {
+      A->split_bd_h = bd;
       in.insert(in.end(), bd.begin(), bd.end());
       e = hipMalloc(&A->d_split, in.size() * sizeof(int));
       if (e == hipSuccess)
         e = hipMemcpyAsync(A->d_split, in.data(), in.size() * sizeof(int), hipMemcpyHostToDevice,
                            s);
       if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e == hipSuccess && ctx->cstream) e = hipEventCreateWithFlags(&A->ev_pack, hipEventDisableTiming);
-      if (e == hipSuccess && ctx->cstream) e = hipEventCreateWithFlags(&A->ev_halo, hipEventDisableTiming);
+      if (e == hipSuccess && ctx->cstream && !A->ev_pack)
+        e = hipEventCreateWithFlags(&A->ev_pack, hipEventDisableTiming);
+      if (e == hipSuccess && ctx->cstream && !A->ev_halo)
+        e = hipEventCreateWithFlags(&A->ev_halo, hipEventDisableTiming);
       if (e != hipSuccess) {
         cgx_csr_destroy(A);
         return hip_fail(e, "cgx_csr_create_dist(slice split)");
@@ -694,13 +698,18 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
         }
         A->bnd_nblk = (int)blk.size();
       }
-      // a lean loop SpMV walks the interior only (the boundary slices are the
-      // boundary launch's)
-      if ((rc = lean_mark_split(A, bd))) {
-        cgx_csr_destroy(A);
-        return rc;
-      }
     }
+  }
+  if ((rc = autotune_spmv(A))) {
+    cgx_csr_destroy(A);
+    return rc;
+  }
+  if (!A->dev.sl) A->split_bd_h.clear();  // a CSR-stream form won: no split
+  // a lean loop SpMV walks the interior only (the boundary slices are the
+  // boundary launch's)
+  if (A->split_ni > 0 && (rc = lean_mark_split(A, A->split_bd_h))) {
+    cgx_csr_destroy(A);
+    return rc;
   }
   *out = A;
   return CGX_OK;

@@ -179,6 +179,14 @@ struct cgx_csr {
   int *d_bnd_blk = nullptr;
   int bnd_nblk = 0;
   bool split_ordered = false;  // interior list in the chunked visit order
+  std::vector<int> split_bd_h;  // the boundary slices (host copy: the lean walk's 0xfe marks)
+  // the SpMV autotune's record (cgx_abi.cpp autotune_spmv): every form timed,
+  // how (CGX_TUNE_* of cgx.h) and its median µs per launch
+  struct TuneRec {
+    int variant, kind;
+    float us;
+  };
+  std::vector<TuneRec> tune;
   hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
   cgx::Peer peer;  // device peer transport (cgx_dist_peer_enable)
   int64_t sell_padded = 0;

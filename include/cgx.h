@@ -135,6 +135,20 @@ int cgx_csr_templates(cgx_csr *csr, int *n_templates, int64_t *slices);
  * VectorOperations.hpp:438-466's SpMV. */
 int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, int *D, int *a,
                       int *chunked);
+/* The SpMV autotune's record of this matrix (cgx_csr_create /
+ * cgx_csr_create_dist): every form it timed, how it was timed and its median
+ * µs per launch over the interleaved rounds; *count = the record's length
+ * (0 when a variant was forced or the matrix is small enough for the size
+ * rule). Up to `cap` entries are written. A form displaces the preferred
+ * (more specialised) one only when at least 3% faster. Replaces nothing in
+ * the reference (its SpMV has one form, VectorOperations.hpp:438-466). */
+#define CGX_TUNE_DOT 0          /* k_spmv_dot over the whole matrix */
+#define CGX_TUNE_DOT_INTERIOR 1 /* k_spmv_dot over a split matrix's interior slices */
+#define CGX_TUNE_FD 2           /* k_spmv_fd (mode 4's SpMV; 2-D plane march) */
+#define CGX_TUNE_LEAN 3         /* the lean walk over the whole matrix */
+#define CGX_TUNE_LEAN_INTERIOR 4 /* the lean walk over a split matrix's interior */
+int cgx_csr_autotune_record(cgx_csr *csr, int *variants, int *kinds, float *us, int cap,
+                            int *count);
 /* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
  * *stride = slices (of 128 rows) between a slice and its +-D neighbour
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D

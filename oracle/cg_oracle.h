@@ -84,7 +84,12 @@ double orc_accuracy(int64_t n, const int *rowptr, const int *col,
 /* CPU baseline: the same per-iteration command sequence as CG.hpp:359-436,
  * with every parallel_for run as an OpenMP loop on `threads` threads (the
  * AdaptiveCpp OpenMP backend's execution model). Runs exactly `iters` loop
- * bodies, no stop test. Returns wall seconds of the iteration loop only. */
+ * bodies, no stop test. Returns wall seconds of the iteration loop only.
+ * orc_cg_timed_omp runs `warmup` untimed bodies before the `iters` timed
+ * ones (the SURVEY 8(d) protocol: K = 500 after 20 warm-up). */
+double orc_cg_timed_omp(int64_t n, const int *rowptr, const int *col, const double *val,
+                        const double *b, double *x, int64_t warmup, int64_t iters,
+                        int threads);
 double orc_cg_fixed_iters_omp(int64_t n, const int *rowptr, const int *col,
                               const double *val, const double *b, double *x,
                               int64_t iters, int threads);

@@ -68,6 +68,8 @@ def lib() -> C.CDLL:
         L.orc_accuracy.restype = C.c_double
         L.orc_cg_fixed_iters_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [_i64, C.c_int]
         L.orc_cg_fixed_iters_omp.restype = C.c_double
+        L.orc_cg_timed_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [_i64, _i64, C.c_int]
+        L.orc_cg_timed_omp.restype = C.c_double
         L.orc_cg_solve_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [C.c_int, C.c_double, _i64,
                                                                    C.c_int, C.POINTER(CgResult)]
         L.orc_cg_solve_omp.restype = C.c_int
@@ -194,6 +196,16 @@ def cg_fixed_iters_omp(rowptr, col, val, b, iters: int, threads: int):
     x = np.zeros(n)
     t = lib().orc_cg_fixed_iters_omp(n, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(b), _ptr(x),
                                      iters, threads)
+    return t, x
+
+
+def cg_timed_omp(rowptr, col, val, b, warmup: int, iters: int, threads: int):
+    """CPU baseline with `warmup` untimed bodies first: returns (seconds of
+    the `iters` timed bodies, x)."""
+    n = len(rowptr) - 1
+    x = np.zeros(n)
+    t = lib().orc_cg_timed_omp(n, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(b), _ptr(x),
+                               warmup, iters, threads)
     return t, x
 
 

@@ -72,6 +72,13 @@ def test_512cubed_matches_oracle(queue, oracle):
     m = cga.Matrix.poisson(queue, 3, 512, 512, 512)
     assert m.N() == n and m.NNZ() == len(vl)
     prod = _variant(m)
+    # the benchmarked 512^3 kernel: the lean walk, chunked (planes of 2,048
+    # slices are four grid steps wide)
+    assert prod & 33554432, f"512^3 autotune picked {prod}, not the lean walk"
+    c, s_, g, d, a, chunked = C.c_int(), C.c_int64(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(lib().cgx_csr_lean_info(m.schedule(), C.byref(c), C.byref(s_), C.byref(g), C.byref(d),
+                                  C.byref(a), C.byref(chunked)))
+    assert chunked.value == 1 and d.value == 512 * 512, (chunked.value, d.value)
     x = np.random.default_rng(5120).standard_normal(n)
     y = cga.Vector(queue, n)
     cga.VectorOperations(queue).spmv(m, cga.Vector(queue, x), y, m.NNZ(), count=n)

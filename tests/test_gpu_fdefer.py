@@ -51,6 +51,9 @@ CASES = [
     ("3d-full", (3, 256, 256, 256), None),
     ("3d-march", (3, 128, 128, 24), 3973122),
     ("sellp", (3, 48, 48, 30), 8194),
+    # the lean walk forced (k_spmv_fd_lean: p_k formed in the gathers, the
+    # formed +-D pairs carried in registers)
+    ("3d-lean", (3, 128, 48, 40), "33554432:0"),
     ("csr-stream", (3, 48, 48, 30), 13),
 ]
 
@@ -60,6 +63,8 @@ def test_mode4_bit_identical_to_mode1(queue, oracle, monkeypatch, name, dims, va
     if variant is not None:
         monkeypatch.setenv("CGX_SPMV_VARIANT", str(variant))
     m = cga.Matrix.poisson(queue, *dims)
+    if name == "3d-lean":
+        assert _variant(m) & 33554432
     n = m.N()
     gf, gs = C.c_int(), C.c_int()
     check(lib().cgx_csr_fd_grid(m.schedule(), C.byref(gf), C.byref(gs)))

@@ -30,6 +30,20 @@ pytestmark = pytest.mark.gpu
 
 CONFIGS = {"poisson2d_4096": (2, 4096, 4096, 1), "poisson3d_256": (3, 256, 256, 256)}
 BODIES = 40
+KVL = 33554432  # the lean stencil walk's variant bit (include/cgx.h cgx_csr_lean_info)
+
+
+def _variant(m):
+    v = C.c_int(0)
+    check(lib().cgx_csr_variant(m.schedule(), C.byref(v)))
+    return v.value
+
+
+def _lean_grid(m):
+    c, s, g, d, a, pp = C.c_int(), C.c_int64(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(lib().cgx_csr_lean_info(m.schedule(), C.byref(c), C.byref(s), C.byref(g),
+                                  C.byref(d), C.byref(a), C.byref(pp)))
+    return g.value, pp.value
 
 
 @pytest.fixture(scope="module", params=sorted(CONFIGS))
@@ -51,9 +65,8 @@ def test_fullsize_generator_matches_oracle(full):
 
 def test_fullsize_spmv_bitexact_in_production_format(queue, oracle, full):
     name, m, (rp, cl, vl) = full
-    variant = C.c_int(0)
-    check(lib().cgx_csr_variant(m.schedule(), C.byref(variant)))
-    assert variant.value & 8192, f"{name}: expected the SELL-P format, got {variant.value}"
+    variant = _variant(m)
+    assert variant & 8192, f"{name}: expected the SELL-P format, got {variant}"
     n = m.N()
     x = np.random.default_rng(11).standard_normal(n)
     xv = cga.Vector(queue, x)
@@ -71,6 +84,36 @@ def _bodies(queue, m, b, mode):
     cg.solve(0.0, max_iter=BODIES)
     assert cg.iterations == BODIES
     return cg
+
+
+def test_fullsize_benchmarked_lean_walk_pinned(queue, oracle, full, monkeypatch):
+    """The kernel bench.py's 256^3 line times (k_spmv_lean, the lean stencil
+    walk at its plane-matched grid) is the autotune's choice there, and the
+    same walk forced at creation ($CGX_SPMV_VARIANT=kVL:0, whatever the
+    timing on this box) is bit-exact against the oracle's per-row loop and
+    carries 40 CG bodies to the oracle's iterates in modes 3, 1 and 4."""
+    name, m, (rp, cl, vl) = full
+    if name != "poisson3d_256":
+        pytest.skip("the lean walk is the 3-D headline's format (4096^2 runs the plane march)")
+    prod = _variant(m)
+    assert prod & KVL, f"256^3 autotune picked {prod}, not the lean walk"
+    monkeypatch.setenv("CGX_SPMV_VARIANT", f"{KVL}:0")
+    mf = cga.Matrix.poisson(queue, 3, 256, 256, 256)
+    assert _variant(mf) == prod
+    assert _lean_grid(mf) == _lean_grid(m) == (1024, 0)  # plane-matched, no chunking
+    n = mf.N()
+    x = np.random.default_rng(256).standard_normal(n)
+    y = cga.Vector(queue, n)
+    cga.VectorOperations(queue).spmv(mf, cga.Vector(queue, x), y, mf.NNZ(), count=n)
+    np.testing.assert_array_equal(y.to_numpy(), oracle.spmv(rp, cl, vl, x))
+    del y
+    b = np.arange(1, n + 1, dtype=np.float64)  # Tester.cpp:27-30
+    xs = {mode: _bodies(queue, mf, b, mode).extract() for mode in (3, 1, 4)}
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, BODIES, 16)
+    assert rel(xs[3], xr) <= 1e-10, rel(xs[3], xr)
+    np.testing.assert_array_equal(xs[3], xs[1])
+    # mode 4's fused walk runs on the walk's own grid: the same p.Ap partials
+    np.testing.assert_array_equal(xs[4], xs[1])
 
 
 def test_fullsize_cg_bodies_match_oracle(queue, oracle, full):

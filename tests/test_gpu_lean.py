@@ -122,7 +122,7 @@ def test_lean_refused_without_templates(queue, oracle, monkeypatch):
         check(lib().cgx_csr_set_variant(m.schedule(), KVL))
 
 
-@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("mode", [1, 3, 4])
 def test_lean_in_the_solver(queue, oracle, mode):
     dims = (3, 128, 64, 40)
     rp, cl, vl = oracle.poisson(*dims)
@@ -147,19 +147,32 @@ def test_lean_in_the_solver(queue, oracle, mode):
 
 
 def test_lean_modes_3_and_1_bit_identical(queue, oracle):
+    """Modes 3 and 4 (x deferred over four bodies; mode 4 forms p_k inside
+    k_spmv_fd_lean, on the walk's own grid) against mode 1, solved to
+    tolerances whose body counts end in every slot of a 4-body group: body
+    count, x and final r.r bit for bit, and the oracle's body count."""
     rp, cl, vl = oracle.poisson(3, 128, 64, 40)
     n = len(rp) - 1
     b = np.arange(1, n + 1, dtype=np.float64)
-    out = []
-    for mode in (1, 3):
-        m = Matrix(queue, vl, cl, rp)
-        check(lib().cgx_csr_set_sell(m.schedule(), 3))
-        check(lib().cgx_csr_set_variant(m.schedule(), KVL))
-        cg = CG(queue)
-        cg.mode = mode
-        cg.setMatrix(m)
-        cg.setTarget(b)
-        cg.solve(1e-8 * float(np.linalg.norm(b)))
-        out.append((cg.iterations, cg.extract()))
-    assert out[0][0] == out[1][0]
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    m = Matrix(queue, vl, cl, rp)
+    check(lib().cgx_csr_set_sell(m.schedule(), 3))
+    check(lib().cgx_csr_set_variant(m.schedule(), KVL))
+    slots = set()
+    for tol in (1e-4, 3e-6, 1e-7, 1e-8, 3e-9, 1e-10):
+        out = {}
+        for mode in (1, 3, 4):
+            cg = CG(queue)
+            cg.mode = mode
+            cg.setMatrix(m)
+            cg.setTarget(b)
+            cg.solve(tol * float(np.linalg.norm(b)))
+            out[mode] = (cg.iterations, cg.extract(), cg.final_rxr)
+        for mode in (3, 4):
+            assert out[mode][0] == out[1][0], (tol, mode)
+            np.testing.assert_array_equal(out[mode][1], out[1][1])
+            assert out[mode][2] == out[1][2]
+        slots.add(out[1][0] % 4)
+        if tol == 1e-8:
+            _, res = oracle.cg_solve_omp(rp, cl, vl, b, tol * float(np.linalg.norm(b)), 8)
+            assert abs(out[1][0] - res.iterations) <= 2
+    assert len(slots) >= 3, slots
