@@ -3342,15 +3342,9 @@ __global__ __launch_bounds__(kBlock) void k_flush_defer(int64_t n, T *__restrict
     any = any || use[t];
   }
   if (!any) return;
-  const T *Ps[4] = {P0, P1, P2, P3};
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    T xv = x[i];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (use[t]) xv = xv + a[t] * Ps[t][i];
-    x[i] = xv;
-  }
+  // 16-byte lanes, the group flush's loop (the end of the driver's 20-body
+  // bench window pays this launch: 8-byte lanes took 75.6 us at 256^3, r04d)
+  flush_group_range<T>(n, x, P0, P1, P2, P3, a, use, 0);
 }
 
 template <typename T>
@@ -3988,7 +3982,7 @@ hipError_t Launch<T>::update_p_defer(int64_t n, T *x, const T *p, T *pn, T *cons
 template <typename T>
 hipError_t Launch<T>::flush_defer(int64_t n, T *x, T *const P[4], CgScalars<T> *st,
                                   hipStream_t s) {
-  CGX_GGL(k_flush_defer<T>, dim3(elem_grid(n, 4)), dim3(kBlock), 0, s, n, x,
+  CGX_GGL(k_flush_defer<T>, dim3(grid_elems(n, kGridUpdateP)), dim3(kBlock), 0, s, n, x,
                      (const T *)P[0], (const T *)P[1], (const T *)P[2], (const T *)P[3],
                      (const CgScalars<T> *)st);
   hipError_t e = hipGetLastError();

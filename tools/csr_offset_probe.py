@@ -44,10 +44,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--create", type=int, default=0,
+                    help="variant forced at creation (default: --variant)")
     ap.add_argument("--layouts", default=",".join(LAYOUTS),
                     help="names from LAYOUTS, or v:c:r:p:y byte offsets (K / M suffixes)")
     a = ap.parse_args()
-    os.environ["CGX_SPMV_VARIANT"] = str(a.variant)
+    os.environ["CGX_SPMV_VARIANT"] = str(a.create or a.variant)
     L = lib()
     q = cga.Queue(0)
     nx = a.n
@@ -61,8 +63,8 @@ def main():
         return int(t[:-1] if mul > 1 else t) * mul
 
     for name in a.layouts.split(","):
-        if name not in LAYOUTS:
-            LAYOUTS[name] = tuple(nbytes(t) for t in name.split(":"))
+        if name not in LAYOUTS:  # "v:c:r:p:y", or "v:c:r:p:y#k" for a repeat
+            LAYOUTS[name] = tuple(nbytes(t) for t in name.split("#")[0].split(":"))
         ov, oc, orp, op, oy = LAYOUTS[name]
         val = cga.DeviceArray(q, nnz * 8 + PAD, np.uint8)
         col = cga.DeviceArray(q, nnz * 4 + PAD, np.uint8)
@@ -92,6 +94,7 @@ def main():
             ref = out
         t = np.array(times[name])
         print(json.dumps({"layout": name, "offsets": LAYOUTS[name], "variant": a.variant,
+                          "bases": [hex(bf.ptr) for bf in bufs],
                           "median_us": round(float(np.median(t)), 2),
                           "min_us": round(float(t.min()), 2),
                           "max_us": round(float(t.max()), 2),
