@@ -131,6 +131,8 @@ def parse(argv=None):
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC passes that measure roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--lean-team", choices=["auto", "0", "1"], default="auto",
+                    help=argparse.SUPPRESS)  # A/B: the lean walk's team form off / on
     ap.add_argument("--master-port", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -263,7 +265,8 @@ def cpu_baseline(workload: str, grid, threads: int, budget_s: float, iters: int 
 
 
 TUNE_KINDS = {0: "k_spmv_dot", 1: "k_spmv_dot (interior slices)", 2: "k_spmv_fd",
-              3: "lean walk", 4: "lean walk (interior slices)"}
+              3: "lean walk", 4: "lean walk (interior slices)",
+              5: "k_spmv_fd lean walk, team form"}
 
 
 def autotune_record(L, A) -> dict | None:
@@ -430,6 +433,8 @@ def run(args) -> None:
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, wl.rows.ptr, wl.cols.ptr,
                                wl.vals.ptr, F64, None, C.byref(A)))
+    if args.lean_team in ("0", "1") and not dist_on:  # A/B of the lean walk's team form
+        check(L.cgx_csr_set_lean_team(A, int(args.lean_team)))
     peer_note = None
     validation = None
     use_peer = world > 1 and args.transport in ("peer", "host-peer")
@@ -466,6 +471,10 @@ def run(args) -> None:
     lean = [C.c_int(0), C.c_int64(0), C.c_int(0), C.c_int(0), C.c_int(0), C.c_int(0)]
     check(L.cgx_csr_lean_info(A, *[C.byref(v) for v in lean]))
     lean_on = bool(variant.value & KVL)
+    team = C.c_int(0)
+    if lean_on and hasattr(L, "cgx_csr_lean_team"):
+        check(L.cgx_csr_lean_team(A, C.byref(team)))
+    sfx = "_t" if team.value else ""  # the walk's team form (1,024-thread workgroups)
     autotune = autotune_record(L, A)
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
@@ -554,7 +563,7 @@ def run(args) -> None:
         ach = kb / (avg[1] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
             (16 * n_local if mode_eff == 4 else 0)
-        kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" if lean_on else "k_spmv_fd"}.get(
+        kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" + sfx if lean_on else "k_spmv_fd"}.get(
             mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
@@ -580,10 +589,10 @@ def run(args) -> None:
             # workload, variant and mode (child processes, after this run)
             # (a lean walk is forced at the grid its class layout was built for)
             t = pmc_traffic(args, f"{int(variant.value)}:{lean[2].value}" if lean_on
-                            else str(int(variant.value)), mode_eff)
+                            else str(int(variant.value)), mode_eff, team.value)
             roof["traffic_by_kernel"] = t.get("by_kernel")
             roof["traffic_method"] = t.get("method")
-            key = (f"{kname}<double>" if kname in ("k_spmv_lean", "k_spmv_fd_lean")
+            key = (f"{kname}<double>" if kname.startswith(("k_spmv_lean", "k_spmv_fd_lean"))
                    else f"{kname}<double, {int(variant.value & ~KVL)}>")
             if t.get("by_kernel") and key in t["by_kernel"]:
                 roof["traffic"] = t["by_kernel"][key]
@@ -657,7 +666,8 @@ def run(args) -> None:
                            {"classes": lean[0].value, "slices": lean[1].value,
                             "slices_total": (n_local + 127) // 128, "grid": lean[2].value,
                             "D": lean[3].value, "a": lean[4].value,
-                            "chunked_walk": bool(lean[5].value), "in_use": lean_on}
+                            "chunked_walk": bool(lean[5].value), "in_use": lean_on,
+                            "team_form": bool(team.value)}
                            if lean[0].value else None)},
             "roofline": roof,
             "csr_general": general,
@@ -728,7 +738,7 @@ def pmc_bytes(sums: dict) -> dict:
     return out
 
 
-def pmc_traffic(args, variant: str, mode: int, timeout_s: float = 180.0) -> dict:
+def pmc_traffic(args, variant: str, mode: int, team: int = 0, timeout_s: float = 180.0) -> dict:
     """HBM bytes per launch of every kernel of the iteration, from two
     rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE: one counter group per
     run, kernel dispatch counters only) of a short child run of this same
@@ -747,7 +757,8 @@ def pmc_traffic(args, variant: str, mode: int, timeout_s: float = 180.0) -> dict
         return {"error": "rocprofv3 not found"}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
              "--steps", "10", "--warmup", "2", "--profile-steps", "0", "--no-cpu",
-             "--no-general", "--no-traffic", "--mode", str(mode), "--poll", str(args.poll)]
+             "--no-general", "--no-traffic", "--mode", str(mode), "--poll", str(args.poll),
+             "--lean-team", str(int(team))]
     if args.grid:
         child += ["--grid", str(args.grid)]
     env = dict(os.environ, CGX_SPMV_VARIANT=variant)

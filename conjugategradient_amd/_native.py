@@ -74,6 +74,8 @@ _SIGS = {
                                  C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "cgx_csr_autotune_record": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32),
                                        C.POINTER(C.c_float), _i32, C.POINTER(_i32)]),
+    "cgx_csr_set_lean_team": (_i32, [_vp, _i32]),
+    "cgx_csr_lean_team": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_march_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "cgx_csr_stream_bytes": (_i32, [_vp, C.POINTER(C.c_int64)]),
     "cgx_csr_info": (_i32, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),

@@ -1116,7 +1116,7 @@ void free_lean(cgx_csr *A) {
   A->dev.vl_cls = nullptr;
   A->dev.vl_tab = nullptr;
   A->dev.vl_grid = A->dev.vl_nst = A->dev.vl_D = A->dev.vl_a = 0;
-  A->dev.vl_P = A->dev.vl_K = A->dev.vl_lds = A->dev.vl_split = 0;
+  A->dev.vl_P = A->dev.vl_K = A->dev.vl_lds = A->dev.vl_split = A->dev.vl_team = 0;
   A->vl_tab_h.clear();
   A->dev.lean = false;
   A->vl_slice_cls.clear();
@@ -2112,6 +2112,23 @@ extern "C" int cgx_csr_autotune_record(cgx_csr *A, int *variants, int *kinds, fl
   return CGX_OK;
 }
 
+extern "C" int cgx_csr_set_lean_team(cgx_csr *A, int on) {
+  CGX_REQUIRE(A, CGX_EINVAL, "A is NULL");
+  CGX_REQUIRE(!on || (A->dev.vl_cls && !A->dev.vl_split && !A->dev.sell_partial &&
+                      A->dev.vl_grid % 32 == 0 && A->dtype == CGX_F64),
+              CGX_EUNSUPPORTED,
+              "the team walk needs an f64 whole-matrix lean layout whose grid is a multiple "
+              "of 32");
+  A->dev.vl_team = on ? 1 : 0;
+  return CGX_OK;
+}
+
+extern "C" int cgx_csr_lean_team(cgx_csr *A, int *on) {
+  CGX_REQUIRE(A && on, CGX_EINVAL, "NULL argument");
+  *on = A->dev.vl_cls && A->dev.vl_team ? 1 : 0;
+  return CGX_OK;
+}
+
 extern "C" int cgx_csr_march_info(cgx_csr *A, int *stride, int *offset_a, int *run_planes) {
   CGX_REQUIRE(A && stride && offset_a && run_planes, CGX_EINVAL, "NULL argument");
   const bool on = A->dev.svc && A->dev.sell_maxw <= 8 && A->dev.march_k > 0;
@@ -2448,6 +2465,7 @@ int autotune_spmv(cgx_csr *A) {
   // profiles/r04_lean_pipe512.log; not built.)
   std::vector<VlClass> vtab;
   int lean_G = 0;
+  bool lean_team = false;
   // A 2-D plane-march winner runs the loop in mode 4 (fd_auto: two kernels
   // per body, the p update inside the march's SpMV), which the lean walk's
   // mode 3 does not beat (4096^2: 4,983 against 5,187-5,372 it/s,
@@ -2470,6 +2488,18 @@ int autotune_spmv(cgx_csr *A) {
       if (tune_pick(lm) == 0) lean_G = G;
       else best_us = lm[1];
     }
+    // mode 4's fused walk in its team form (a whole-matrix walk whose grid
+    // splits into 1,024-thread workgroups by XCD: G / 4 a multiple of 8),
+    // by rule: where p alone exceeds the Infinity Cache (>= 32 M rows, where
+    // fd_auto runs mode 4). In the loop 512^3 took 1,000 against 1,065 us
+    // (548 against 520 it/s) and 256^3 113 against 127; the 256 x 256 x 32
+    // slab (4 steps per wave) 18.5 against 15.8 (profiles/r05l_team_ab.log).
+    // Timed alone on a warm cache the team form loses (256^3 111 against 97
+    // us, 512^3 1,004 against 821): the isolated timing does not see what it
+    // saves in the loop, so it is not timed here.
+    if (e == hipSuccess && lean_G > 0 && !split && G % 32 == 0 && A->dtype == CGX_F64 &&
+        A->dev.n >= (int64_t(32) << 20))
+      lean_team = true;
   }
   (void)best_us;
   if (e0) (void)hipEventDestroy(e0);
@@ -2487,6 +2517,7 @@ int autotune_spmv(cgx_csr *A) {
     if (int rc = build_lean_layout(A, vtab, lean_G)) return rc;
     A->dev.variant = kVlBase;
     A->dev.lean = true;
+    A->dev.vl_team = lean_team ? 1 : 0;
     return CGX_OK;
   }
   free_lean(A);
@@ -2665,7 +2696,12 @@ static bool fd_auto(const cgx_cg *cg) {
   // 31.9-32.1 in mode 3; at 256^3 mode 3 wins (5,182-5,208 against
   // 4,750-4,807 it/s; profiles/r04_dist_ab.log, r04b_slab.log)
   const bool lean_cached = vl_whole(A->dev) && A->dev.n <= (int64_t(4) << 20);
-  return march2d || (small && (v & 1048576)) || lean_cached;
+  // ... and with p alone past the Infinity Cache (>= 32 M rows: no p line the
+  // p update writes survives to the SpMV, which mode 3's gain at 256^3 is):
+  // 512^3 520 against 508 it/s, 548 with the fused walk's team form
+  // (profiles/r05l_team_ab.log)
+  const bool lean_big = vl_whole(A->dev) && A->dev.n >= (int64_t(32) << 20);
+  return march2d || (small && (v & 1048576)) || lean_cached || lean_big;
 }
 
 // Auto mode picks 5 (the persistent body) for small single-device f64

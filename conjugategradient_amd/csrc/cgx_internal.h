@@ -194,6 +194,11 @@ struct CsrDev {
   // a partitioned matrix's layout: its boundary slices (the split's, run by
   // the boundary launch) are skipped, so the walk covers the interior only
   int vl_split = 0;
+  // mode 4's fused walk (k_spmv_fd_lean) in its team form (1,024-thread
+  // workgroups sharing their neighbours' formed p_k pairs through LDS;
+  // cgx_kernels.hip spmv_lean_team): vl_grid / 4 workgroups; whole-matrix
+  // walks only
+  int vl_team = 0;
   bool lean = false;
   // a partitioned matrix's SELL copy holds its boundary slices only as
   // placeholders (their rows may be unsorted in local numbering: ghosts from

@@ -1858,6 +1858,198 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
   }
 }
 
+// Team form of the lean walk, mode 4's fused kernel only (CsrDev::vl_team;
+// DESIGN.md §4 "team walk"; as the plain SpMV it ran 64-66 against 48 us at
+// 256^3, the per-step barrier costing more than the gathers it saves):
+// one 1,024-thread workgroup per CU, its 16 waves at 16 consecutive walk
+// positions of the class layout a 4-wave grid of 4x the workgroups was built
+// for (the same rows of class bytes, the same step). At every step the 16
+// waves hold 16 consecutive slices of one plane (or plane chunk), so a
+// slice's +-a neighbours (a / 128 slices away) and its x-line's outer
+// neighbours (one slice away) are, but for the team's edge waves, another
+// wave's center pair of the same step: each wave publishes its center pair to
+// LDS, one LDS barrier, and reads those pairs from there instead of
+// gathering them (their L1 -> L2 requests are what the walk's requests beyond
+// the compulsory center lines are: PMC). With GatherP (mode 4)
+// the published pairs are the formed p_k, so a neighbour's pair costs no r /
+// p_{k-1} loads either. Per row the same products in the same order as the
+// 4-wave walk: Ap bit for bit.
+constexpr int kTeamWaves = 16;
+constexpr int kTeamBlock = 64 * kTeamWaves;
+template <typename T> struct TeamLds {
+  typename PairU<T>::V pub[2][kTeamWaves][64];  // published centers, double-buffered by step
+  SellLds<T> sell;                              // the per-slice form's dictionary, reductions
+  T red[kTeamWaves];
+};
+
+template <typename T, class Epi, class Gather>
+__device__ __forceinline__ void spmv_lean_team(const CsrArgs &A, const Gather &x, Epi &epi,
+                                               const T *__restrict__ vd,
+                                               const unsigned long long *vt, TeamLds<T> &tl) {
+  constexpr int VG = 8192 | 32768 | 262144 | 524288 | kVT | 2;  // the generic slices' form
+  using PV = decltype(x.pair_b(0u));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int Gt = (int)gridDim.x, b = (int)blockIdx.x, g = b & 7;
+  const int step = (Gt >> 3) * kTeamWaves;  // the layout grid's G / 2
+  const int w0 = (b >> 3) * kTeamWaves, w = w0 + wid;
+  const int nsl = (int)A.nsl;
+  const int lo = (int)(((int64_t)nsl * g) >> 3), end = (int)(((int64_t)nsl * (g + 1)) >> 3);
+  const unsigned *__restrict__ row = reinterpret_cast<const unsigned *>(
+      A.vl_cls + (int64_t)((A.rev ? 8 * step : 0) + g * step + w) * A.vl_nst);
+  const int nw = A.vl_nst >> 2;
+  const auto *tab = (const __attribute__((address_space(4))) VlClass *)A.vl_tab;
+  const unsigned oD = (unsigned)A.vl_D * (unsigned)sizeof(T);
+  const unsigned oa = (unsigned)A.vl_a * (unsigned)sizeof(T);
+  const int P = A.vl_P, K = A.vl_K;
+  const int D = A.vl_D, a = A.vl_a;
+  const int nxi = (int)A.nx;
+  const int Kp = D / (2 * kSellRows);
+  const bool carry_walk = D % (2 * kSellRows) == 0 && (P > 0 ? K == Kp : step == Kp);
+  // the +-a neighbours' walk offset (0: not whole slices, always gathered)
+  const int asl = (a > 0 && a % (2 * kSellRows) == 0) ? a / (2 * kSellRows) : 0;
+  // trips: every wave of the team takes the same number (one barrier each);
+  // the plane-matched walk's last trip may leave the higher waves idle
+  const int trips = P > 0 ? (K / step) * P : (end - lo - w0 + step - 1) / step;
+  int zp = 0, cb = 0;
+  int s = lo + w;
+  unsigned cw = 0;
+  PV c_ahead, c_ct;
+  int carry_s = -1;
+  for (int j = 0; j < trips; ++j) {
+    if ((j & 255) == 0) {
+      const int k = (j >> 2) + lane;
+      cw = k < nw ? row[k] : ~0u;
+      asm volatile("" : "+v"(cw));
+    }
+    const bool act = s < end;
+    const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, (j & 255) >> 2);
+    const int c = act ? (int)((word >> (8 * (j & 3))) & 0xffu) : 0xfe;
+    const int si = A.rev ? lo + end - 1 - s : s;
+    const int fr = si * (2 * kSellRows);
+    const int r0 = fr + 2 * lane;
+    const unsigned rb = (unsigned)r0 * (unsigned)sizeof(T);
+    const unsigned omD = rb - (fr >= D ? oD : 0u);
+    const unsigned opD = rb + (fr + 2 * kSellRows + D <= nxi ? oD : 0u);
+    const int buf = j & 1;
+    PV ct, behind, ahead;
+    if (c < 0xfe) {
+      if (s == carry_s) {
+        ct = c_ahead;
+        behind = c_ct;
+      } else {
+        ct = x.pair_b(rb);
+        behind = x.pair_b(A.rev ? opD : omD);
+      }
+      ahead = x.pair_b(A.rev ? omD : opD);
+      tl.pub[buf][wid][lane] = ct;
+    } else if (c == 0xff) {
+      tl.pub[buf][wid][lane] = x.pair_b(rb);  // the neighbours' pairs
+    }
+    lds_barrier();
+    if (c == 0xff) {
+      sellpv_slice2<T, VG, Epi, Gather>(A, x, epi, vd, si, vt);
+    } else if (c < 0xfe) {
+      // the neighbour waves at this step (the same trip: positions +-1, +-asl
+      // away) where they are in the team and active, else a gather
+      const int dm = A.rev ? 1 : -1;  // the walk offset of the slice before this one
+      auto in_team = [&](int off) {
+        const int x2 = wid + off;
+        return x2 >= 0 && x2 < kTeamWaves && s + off >= lo && s + off < end;
+      };
+      T elo, ehi;
+      if (fr > 0 && in_team(dm))
+        elo = tl.pub[buf][wid + dm][63].y;
+      else
+        elo = x.at_s(fr > 0 ? fr - 1 : 0);
+      if (fr + 2 * kSellRows < nxi && in_team(-dm))
+        ehi = tl.pub[buf][wid - dm][0].x;
+      else
+        ehi = x.at_s(fr + 2 * kSellRows < nxi ? fr + 2 * kSellRows : nxi - 1);
+      PV gma, gpa;
+      const bool ma = a > 0 && fr >= a, pa = a > 0 && fr + 2 * kSellRows + a <= nxi;
+      if (ma && asl > 0 && in_team(dm * asl)) gma = tl.pub[buf][wid + dm * asl][lane];
+      else gma = x.pair_b(rb - (ma ? oa : 0u));
+      if (pa && asl > 0 && in_team(-dm * asl)) gpa = tl.pub[buf][wid - dm * asl][lane];
+      else gpa = x.pair_b(rb + (pa ? oa : 0u));
+      const PV gmD = A.rev ? ahead : behind;
+      const PV gpD = A.rev ? behind : ahead;
+      c_ahead = ahead;
+      c_ct = ct;
+      carry_s = carry_walk ? s + Kp : -1;
+      const int pres = tab[c].pres;
+      T v[7];
+#pragma unroll
+      for (int q = 0; q < 7; ++q) v[q] = T(tab[c].v[q]);
+      const T lo_e = tab[c].plo ? elo : -__builtin_copysign(T(0), v[2]);
+      const T hi_e = tab[c].phi ? ehi : -__builtin_copysign(T(0), v[4]);
+      const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
+      epi.pre2c(r0, r0 + 1, ct.x, ct.y);
+      T a0 = T(0), a1 = T(0);
+      if (pres & 1) {
+        a0 = a0 + v[0] * gmD.x;
+        a1 = a1 + v[0] * gmD.y;
+      }
+      if (pres & 2) {
+        a0 = a0 + v[1] * gma.x;
+        a1 = a1 + v[1] * gma.y;
+      }
+      a0 = a0 + v[2] * left;
+      a1 = a1 + v[2] * ct.x;
+      a0 = a0 + v[3] * ct.x;
+      a1 = a1 + v[3] * ct.y;
+      a0 = a0 + v[4] * ct.y;
+      a1 = a1 + v[4] * right;
+      if (pres & 4) {
+        a0 = a0 + v[5] * gpa.x;
+        a1 = a1 + v[5] * gpa.y;
+      }
+      if (pres & 8) {
+        a0 = a0 + v[6] * gpD.x;
+        a1 = a1 + v[6] * gpD.y;
+      }
+      epi.row2(r0, a0, a1, true, true);
+    }
+    // the next position (the plane-matched walk: one step; the chunked walk:
+    // the next plane of the chunk, then the next chunk)
+    if (P == 0) {
+      s += step;
+    } else {
+      if (++zp == P) {
+        zp = 0;
+        cb += step;
+      }
+      s = cb >= K ? end : lo + zp * K + cb + w;
+    }
+  }
+}
+
+// the team's fixed-order sum of one value per thread (valid in thread 0)
+template <typename T> __device__ __forceinline__ T team_sum(T v, T *red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T s = T(0);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int i = 0; i < kTeamWaves; ++i) s = s + red[i];
+  return s;
+}
+// sum_parts's value (its order: threads 0..255 as a 256-thread workgroup)
+// in a team workgroup
+template <typename T> __device__ __forceinline__ T team_sum_parts(const T *part, int np, T *red) {
+  __shared__ T bc;
+  T v = T(0);
+  if (threadIdx.x < kBlock)
+    for (int i = threadIdx.x; i < np; i += kBlock) v += part[i];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0 && threadIdx.x < kBlock) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) bc = ((red[0] + red[1]) + red[2]) + red[3];
+  __syncthreads();
+  return bc;
+}
+
 // LDS layout of a variant's kernel
 template <typename T, int V> struct LdsSel { using type = SpmvLds<T, TileOf<V>::tile>; };
 template <typename T, int V>
@@ -2351,6 +2543,53 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
   T v[1] = {e.acc};
   block_sum<T, 1>(v, sm.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
+// k_spmv_fd_lean in the team form (CsrDev::vl_team): the published centers
+// are the formed p_k, so an in-team neighbour costs no r / p_{k-1} loads
+template <typename T>
+__global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
+    CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
+    T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr) {
+  __shared__ TeamLds<T> tl;
+  const int prev = (slot + 3) & 3;
+  const long long bodies = st->bodies;
+  const bool act = st->active[slot] != 0;
+  if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+  if (!act) {
+    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot) {
+      const T rr = team_sum_parts(ws->rr_part, np_rr, tl.red);
+      if (threadIdx.x == 0) {
+        st->rr[prev] = rr;
+        st->rxr[slot] = rr;
+      }
+    }
+    return;
+  }
+  T beta = T(0);
+  if (bodies > 0) {
+    const T rr = team_sum_parts(ws->rr_part, np_rr, tl.red);
+    beta = rr / st->rxr[prev];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->rr[prev] = rr;  // the record
+      st->rxr[slot] = rr;
+    }
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    for (int i = threadIdx.x; i < kVcDict; i += kTeamBlock) tl.sell.vdict[i] = vd[i];
+    for (int i = threadIdx.x; i < A.nvt * 64; i += kTeamBlock) tl.sell.vt[i] = vt[i];
+    __syncthreads();
+    vd = tl.sell.vdict;
+    vt = tl.sell.vt;
+  }
+  const GatherP<T> g{r, pold, beta};
+  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_lean_team<T>(A, g, e, vd, vt, tl);
+  const T v = team_sum(e.acc, tl.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v;
 }
 
 // The final r.r of a mode-4 run that ended on an active body (no kernel 1
@@ -3599,8 +3838,7 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
   CsrArgs a = args(A);
   a.rev = rev;
   if (vl_whole(A)) {  // the lean stencil walk: its own grid (the class layout's)
-    CGX_GGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot,
-                       ws);
+    CGX_GGL(k_spmv_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, Ap, st, slot, ws);
     return hipGetLastError();
   }
   if (A.sell_partial && (spmv_variant<T>(A) & (2048 | 8192))) {
@@ -3757,7 +3995,7 @@ template <typename T> bool Launch<T>::fd_supported(const CsrDev &A) {
 // to rounding (the sum order of one dot), not bit for bit. Holding k_spmv_fd
 // to k_spmv_dot's waves per SIMD instead spilled 20-56 VGPRs to scratch.
 template <typename T> int Launch<T>::fd_parts(const CsrDev &A) {
-  if (vl_whole(A)) return A.vl_grid;
+  if (vl_whole(A)) return A.vl_team ? A.vl_grid / 4 : A.vl_grid;
   const int grid = grid_rows(A.nrb);
   const int r = spmv_fd_resident<T>(spmv_variant<T>(A));
   return (r > 0 && r < grid) ? r : grid;
@@ -3772,8 +4010,12 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   a.rev = rev;
   if constexpr (std::is_same<T, double>::value) {
     if (vl_whole(A)) {  // the lean walk at its class layout's grid
-      CGX_GGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
-                         Ap, st, slot, ws, np_rr);
+      if (A.vl_team)
+        CGX_GGL(k_spmv_fd_lean_t<T>, dim3(A.vl_grid / 4), dim3(kTeamBlock), 0, s, a, r, pold,
+                pc, Ap, st, slot, ws, np_rr);
+      else
+        CGX_GGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc, Ap, st,
+                slot, ws, np_rr);
       return hipGetLastError();
     }
   }

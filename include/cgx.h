@@ -147,8 +147,19 @@ int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, in
 #define CGX_TUNE_FD 2           /* k_spmv_fd (mode 4's SpMV; 2-D plane march) */
 #define CGX_TUNE_LEAN 3         /* the lean walk over the whole matrix */
 #define CGX_TUNE_LEAN_INTERIOR 4 /* the lean walk over a split matrix's interior */
+#define CGX_TUNE_LEAN_TEAM 5     /* mode 4's fused walk, team form (cgx_csr_set_lean_team) */
 int cgx_csr_autotune_record(cgx_csr *csr, int *variants, int *kinds, float *us, int cap,
                             int *count);
+/* Mode 4's fused lean walk (k_spmv_fd_lean) in its team form: 1,024-thread
+ * workgroups whose 16 waves share their slices' formed p_k neighbour pairs
+ * through LDS instead of gathering r and p_{k-1} for them.
+ * on = 1 selects it (grid / 4 workgroups), 0 the 4-wave form; the plain
+ * SpMV always runs the 4-wave walk. CGX_EUNSUPPORTED without an f64
+ * whole-matrix lean layout whose grid is a multiple of 32. The autotune
+ * decides it at creation. Replaces nothing in the reference
+ * (VectorOperations.hpp:438-466 has one SpMV form). */
+int cgx_csr_set_lean_team(cgx_csr *csr, int on);
+int cgx_csr_lean_team(cgx_csr *csr, int *on);
 /* The plane-march plan of the matrix's SELL-P copy (variant bit 2097152):
  * *stride = slices (of 128 rows) between a slice and its +-D neighbour
  * (0: the dominant slice pattern is not a 7-point / 5-point stencil with D

@@ -176,3 +176,51 @@ def test_lean_modes_3_and_1_bit_identical(queue, oracle):
             _, res = oracle.cg_solve_omp(rp, cl, vl, b, tol * float(np.linalg.norm(b)), 8)
             assert abs(out[1][0] - res.iterations) <= 2
     assert len(slots) >= 3, slots
+
+
+def set_team(m, on=1):
+    check(lib().cgx_csr_set_lean_team(m.schedule(), on))
+    t = C.c_int()
+    check(lib().cgx_csr_lean_team(m.schedule(), C.byref(t)))
+    assert t.value == on
+
+
+@pytest.mark.parametrize("dims", [(3, 128, 64, 40), (3, 512, 256, 16)], ids=["plane", "chunked"])
+def test_lean_team_in_the_solver(queue, oracle, monkeypatch, dims):
+    """Mode 4's fused walk in its team form (k_spmv_fd_lean_t: 16 waves per
+    workgroup, the published pairs are the formed p_k): 45 bodies against
+    the oracle's iterates and against mode 1 (its p.Ap partials split over a
+    quarter of the workgroups: one dot summed in another order, so to
+    rounding), the 4-wave form bit for bit where it is the same launch shape
+    (mode 4 without the team form equals mode 1), and a tolerance stop at
+    the oracle's body count."""
+    rp, cl, vl = oracle.poisson(*dims)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)  # Tester.cpp:27-30
+    monkeypatch.setenv("CGX_SPMV_VARIANT", f"{KVL}:0")
+    m = Matrix(queue, vl, cl, rp)
+    xs = {}
+    for mode, team in ((1, 0), (4, 0), (4, 1)):
+        set_team(m, team)
+        cg = CG(queue)
+        cg.mode = mode
+        cg.setMatrix(m)
+        cg.setTarget(b)
+        cg.solve(0.0, max_iter=45)
+        assert cg.iterations == 45
+        xs[(mode, team)] = cg.extract()
+    _, xr = oracle.cg_fixed_iters_omp(rp, cl, vl, b, 45, 8)
+    np.testing.assert_array_equal(xs[(4, 0)], xs[(1, 0)])
+    assert rel(xs[(4, 1)], xr) <= 1e-10, rel(xs[(4, 1)], xr)
+    assert rel(xs[(4, 1)], xs[(1, 0)]) <= 1e-11
+    tol = 1e-8 * float(np.linalg.norm(b))
+    set_team(m, 1)
+    cg = CG(queue)
+    cg.mode = 4
+    cg.setMatrix(m)
+    cg.setTarget(b)
+    cg.solve(tol)
+    x4 = cg.extract()
+    xo, res = oracle.cg_solve_omp(rp, cl, vl, b, tol, 8)
+    assert abs(cg.iterations - res.iterations) <= 2
+    assert rel(x4, xo) <= 1e-10

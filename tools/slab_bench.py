@@ -39,6 +39,9 @@ def main():
         A = cga.Matrix.poisson(q, dim, nx, ny, nz)
         n = A.N()
         sched = A.schedule()
+        team = os.environ.get("CGX_BENCH_TEAM")  # A/B: force the lean walk's team form on / off
+        if team is not None and hasattr(L, "cgx_csr_set_lean_team"):
+            L.cgx_csr_set_lean_team(sched, int(team))
         b = cga.DeviceArray(q, n, np.float64)
         x = cga.DeviceArray(q, n, np.float64)
         check(L.cgx_iota(q.handle, F64, b.ptr, n, 0.0))
@@ -68,6 +71,7 @@ def main():
         check(L.cgx_cg_kernel_exec_times(cg, avg, calls))
         print(json.dumps({"slab": [nx, ny, nz], "dim": dim, "rows": n, "mode": mode.value,
                           "spmv_variant": v.value, "bodies": steps,
+                          "team": os.environ.get("CGX_BENCH_TEAM"),
                           "us_per_body": round(dt / steps * 1e6, 2),
                           "it_per_s": round(steps / dt, 1),
                           "kernel_us": {"spmv": round(avg[1] * 1e3, 2),
