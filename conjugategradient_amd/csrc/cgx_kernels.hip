@@ -3418,10 +3418,31 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   const T rr_st = cst->rr[slot];
   T pl[kPartsPerThread];
   if (np_rr > 0) parts_load_np(ws->rr_part, np_rr, pl);
+  using V = typename Vec2<T>::V;
+  const int64_t n2 = n >> 1;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  // the non-flushing body: this thread's first four elements of p_k and r
+  // go out with the partials, before beta (as update_r's first block), so
+  // their round trip overlaps the partial sum
+  V pv0[4], rv0[4];
+  if constexpr (!FLUSH) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // clamped (p and r have a slack element): no branch
+      const int64_t j = E(min(i + u * stride, n2 > 0 ? n2 - 1 : 0));
+      pv0[u] = ldv<SNT, T>(reinterpret_cast<const V *>(p) + j);
+      rv0[u] = ldv<SNT, T>(reinterpret_cast<const V *>(r) + j);
+    }
+  }
   if (!act) {
     keep(rxr);
     keep(rr_st);
     if (np_rr > 0) keep(pl);
+    if constexpr (!FLUSH) {
+      keep(pv0);
+      keep(rv0);
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
   }
@@ -3452,9 +3473,6 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
       use[t] = st->skip[t] == 0;
     }
   }
-  using V = typename Vec2<T>::V;
-  const int64_t n2 = n >> 1;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
   const V *p2 = reinterpret_cast<const V *>(p);
   V *pn2 = reinterpret_cast<V *>(pn);
   const V *rv2 = reinterpret_cast<const V *>(r);
@@ -3494,8 +3512,20 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
     }
     pn2[i] = o;
   };
-  auto E = [&](int64_t j) { return rev ? n2 - 1 - j : j; };  // sweep direction
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if constexpr (!FLUSH) {
+    // the first block from the early loads (a block past the end: its
+    // clamped loads are not stored)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i + u * stride < n2) {
+        V o;
+        o.x = rv0[u].x + beta * pv0[u].x;
+        o.y = rv0[u].y + beta * pv0[u].y;
+        pn2[E(i + u * stride)] = o;
+      }
+    }
+    i += 4 * stride;
+  }
   for (; i + 3 * stride < n2; i += 4 * stride) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) body(E(i + u * stride));
