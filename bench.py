@@ -433,7 +433,7 @@ def run(args) -> None:
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, wl.rows.ptr, wl.cols.ptr,
                                wl.vals.ptr, F64, None, C.byref(A)))
-    if args.lean_team in ("0", "1") and not dist_on:  # A/B of the lean walk's team form
+    if args.lean_team != "auto" and not dist_on:  # A/B of the lean walk's team form
         check(L.cgx_csr_set_lean_team(A, int(args.lean_team)))
     peer_note = None
     validation = None

@@ -151,6 +151,28 @@ def test_bench_two_ranks_validates_peer_transport():
     assert "RCCL" in line["config"]["rccl_iteration"]["skipped"]
 
 
+def test_bench_two_ranks_autotune_takes_the_lean_interior():
+    """The metric's grid over two ranks (256 x 256 x 128 slabs, past the
+    autotune's size rule): each rank's autotune times the SELL forms and the
+    lean walk on its interior slices (the boundary slices are the boundary
+    launch's) and takes the lean walk, which then carries the partitioned
+    body (the lean candidate used to be timed as CSR-stream)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--grid", "256",
+           "--steps", "20", "--warmup", "5", "--transport", "host-peer", "--no-cpu",
+           "--profile-steps", "0", "--master-port", str(_port())]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = line["config"]
+    assert cfg["spmv_variant"] & 33554432, cfg["spmv_variant"]
+    hows = {f["how"] for f in cfg["spmv_autotune"]["forms"]}
+    assert "lean walk (interior slices)" in hows and "k_spmv_dot (interior slices)" in hows, hows
+    # a split matrix's SELL forms are timed on its interior slices only
+    for f in cfg["spmv_autotune"]["forms"]:
+        if f["variant"] & (2048 | 8192) and f["how"].startswith("k_spmv_dot"):
+            assert f["how"] == "k_spmv_dot (interior slices)", f
+
+
 def test_bench_rccl_iteration_at_world_size_one():
     """--transport rccl at N = 1: the partitioned path over a one-rank RCCL
     communicator (the all-reduces run, no halo), timed as the line's value
