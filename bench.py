@@ -310,7 +310,8 @@ def rccl_timing(L, q, args, wl, b, x, transport, its, elapsed, world, dist) -> d
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A2, C.byref(cg)))
     check(L.cgx_cg_config(cg, args.poll, 0 if args.no_graph else 1))
-    check(L.cgx_cg_set_mode(cg, args.mode))
+    # (partitioned mode 4 needs the device peer transport: RCCL runs mode 3)
+    check(L.cgx_cg_set_mode(cg, 3 if args.mode == 4 else args.mode))
     # its own x: the timed run's cg continues in the profile pass after this
     # (modes 3 / 4 hold deferred x updates for its x)
     import numpy as np
@@ -483,6 +484,8 @@ def run(args) -> None:
     fused = args.mode == 2
     me = C.c_int(0)
     check(L.cgx_cg_get_mode(cg, C.byref(me)))
+    if dist_on and me.value == 4:
+        sfx = "_push"  # partitioned mode 4: the interior walk with the push in front
     mode_eff = me.value
     total = args.warmup + args.steps + args.profile_steps
     check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total))

@@ -363,6 +363,17 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   return CGX_OK;
 }
 
+// Mode 4 on a partitioned matrix (enqueue_iter_fdefer's partitioned body):
+// f64 over the device peer transport, the interior by the lean walk (its
+// layout skips the boundary slices) and the boundary rows as CSR-stream
+// blocks, i.e. the stencil slabs of SURVEY §8(e)
+bool dist_fd_ok(const cgx_csr *A, int dtype) {
+  return A->dist && A->peer.on && dtype == CGX_F64 &&
+         A->halo.n_ghost + A->halo.send_total > 0 && A->split_ni > 0 &&
+         (launch_variant(A->dev, A->dtype) & (2048 | 8192)) && vl_active(A->dev) &&
+         A->dev.vl_split && A->bnd_nblk > 0;
+}
+
 // Fused deferred-x iteration (mode 4, single device): two kernels per body.
 // Kernel 1 computes p_k = r + beta p_{k-1} where the SpMV reads it and
 // stores it into P[k mod 4] (no separate p update: one read of p less per
@@ -378,8 +389,34 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
   T *Ap = (T *)cg->Ap, *r = (T *)cg->r, *x = (T *)cg->x;
   int rc;
   const int npr = Launch<T>::update_parts(cg->n);
-  const int npp = Launch<T>::fd_parts(A->dev);
   const int par = cg->altdir ? (slot & 1) : 0, rpar = cg->altdir ? 1 - par : 0;
+  if (A->dist) {
+    // partitioned (dist_fd_ok: device peer transport, lean interior, boundary
+    // row blocks): kernel 1 the interior walk with the push of the formed p_k
+    // in front, then the boundary rows after the neighbours' pushes, then
+    // update_r with the p.Ap all-reduce, the stop rule and (slot 3) the flush
+    CGX_REQUIRE(dist_fd_ok(A, cg->dtype), CGX_ESTATE,
+                "mode 4 on a partitioned matrix: the device peer transport or the lean "
+                "interior is no longer set up");
+    const PeerDev &PD = A->peer.dev;
+    const int wg0 = PD.nsend * kPushWG;
+    const int gi = A->dev.vl_grid;
+    if ((rc = timed(cg, 1, s, [&] {
+           hipError_t e = Launch<T>::spmv_fd_lean_push(A->dev, r, P[(slot + 3) & 3], P[slot], Ap,
+                                                       st, slot, ws, npr, s, par, PD, wg0);
+           if (e == hipSuccess)
+             e = Launch<T>::spmv_fd_rows_bnd(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, r,
+                                             P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, s, PD);
+           return e;
+         })))
+      return rc;
+    const int npp = gi + Launch<T>::rows_grid(A->dev, A->bnd_nblk);
+    return timed(cg, 2, s, [&] {
+      return Launch<T>::update_r_peer_rule(cg->n, r, Ap, st, slot, ws, npp, rpar, x,
+                                           slot == 3 ? P : nullptr, s, PD);
+    });
+  }
+  const int npp = Launch<T>::fd_parts(A->dev);
   if ((rc = timed(cg, 1, s, [&] {
          return Launch<T>::spmv_fd(A->dev, r, P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, npr,
                                    s, par);
@@ -472,8 +509,13 @@ int flush_pending_x(cgx_cg *cg) {
       if (cg->slot != 0)
         CGX_HIP(Launch<double>::flush_defer(cg->n, (double *)cg->x, P,
                                             (CgScalars<double> *)cg->st, s));
-      CGX_HIP(Launch<double>::rr_settle((CgScalars<double> *)cg->st, (RedWs<double> *)cg->ws, npr,
-                                        s));
+      if (cg->A->dist)  // the world r.r (dist_fd_ok: the device peer transport)
+        CGX_HIP(Launch<double>::rr_settle_peer((CgScalars<double> *)cg->st,
+                                               (RedWs<double> *)cg->ws, npr, s,
+                                               cg->A->peer.dev));
+      else
+        CGX_HIP(Launch<double>::rr_settle((CgScalars<double> *)cg->st, (RedWs<double> *)cg->ws,
+                                          npr, s));
     }
     return CGX_OK;
   }
@@ -2794,13 +2836,18 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
                 (long long)std::min(device_cus(cg), kCoopMaxG) * 1024 * kCoopStreamMaxR,
                 std::min(device_cus(cg), kCoopMaxG), kCoopStreamMaxR, (long long)cg->n);
   }
-  CGX_REQUIRE(!((mode == 2 || mode == 4) && cg->A->dist), CGX_EUNSUPPORTED,
-              "the fused iterations run on a single device (partitioned matrices use mode 1 or 3)");
+  CGX_REQUIRE(!(mode == 2 && cg->A->dist), CGX_EUNSUPPORTED,
+              "the fused iteration (mode 2) runs on a single device");
+  CGX_REQUIRE(!(mode == 4 && cg->A->dist) || dist_fd_ok(cg->A, cg->dtype), CGX_EUNSUPPORTED,
+              "mode 4 on a partitioned matrix needs f64, the device peer transport and the lean "
+              "interior walk with boundary row blocks (partitioned matrices otherwise use mode 1 "
+              "or 3)");
   CGX_REQUIRE(mode != 2 || (cg->dtype == CGX_F32 ? Launch<float>::fused_supported(cg->A->dev)
                                                  : Launch<double>::fused_supported(cg->A->dev)),
               CGX_EUNSUPPORTED, "mode 2 needs a production SpMV format (variant %d has no fused "
               "kernel)", launch_variant(cg->A->dev, cg->dtype));
-  CGX_REQUIRE(mode != 4 || (cg->dtype == CGX_F64 && Launch<double>::fd_supported(cg->A->dev)),
+  CGX_REQUIRE(mode != 4 || cg->A->dist ||
+                  (cg->dtype == CGX_F64 && Launch<double>::fd_supported(cg->A->dev)),
               CGX_EUNSUPPORTED, "mode 4 needs an f64 matrix in a production SpMV format "
               "(variant %d has no fused kernel)", launch_variant(cg->A->dev, cg->dtype));
   if (mode == 0) {

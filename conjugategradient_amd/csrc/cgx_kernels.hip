@@ -500,6 +500,32 @@ template <typename T, bool NTP = false> struct GatherP {
            beta * ((const __attribute__((address_space(4))) T *)pp)[i];
   }
 };
+// Mode 4's boundary rows of a partitioned matrix (k_spmv_fd_bnd): own
+// columns form p_k as GatherP, ghosts (from n on) are the neighbours' formed
+// p_k where their pushes landed (GatherXL's landing buffer)
+template <typename T> struct GatherPL {
+  GatherP<T> g;
+  const T *__restrict__ land;
+  int n;
+  __device__ __forceinline__ T operator()(int c) const { return c < n ? g(c) : land[c - n]; }
+  __device__ __forceinline__ typename PairU<T>::V pair(int c) const {
+    using U = typename PairU<T>::V;
+    if (c + 1 < n) return g.pair(c);
+    if (c >= n) return *reinterpret_cast<const U *>(land + (c - n));
+    U r;
+    r.x = g(c);
+    r.y = land[0];
+    return r;
+  }
+  __device__ __forceinline__ typename PairU<T>::V pair_b(unsigned b) const {
+    return pair((int)(b / (unsigned)sizeof(T)));
+  }
+  __device__ __forceinline__ T at_s(int i) const {
+    if (i < n) return g.at_s(i);
+    return __hip_atomic_load(const_cast<T *>(land + (i - n)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+};
 
 template <int V>
 __device__ __forceinline__ void work_range(int nrb, int &first, int &step, int &end) {
@@ -2291,6 +2317,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
     st->bodies = 0;
     st->cap = cap;
     st->stopped = 0;
+    st->rr_held = 0;
   }
 }
 
@@ -2592,6 +2619,122 @@ __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v;
 }
 
+// Mode 4 on a partitioned matrix (device peer transport), kernel 1 of 3:
+// k_spmv_fd_lean over the interior slices, with the halo push of the formed
+// p_k (the value this rank's own SpMV forms for those rows) in the first
+// A.wg0 workgroups. beta needs the WORLD r.r of body k-1, so every workgroup
+// all-reduces the partials here (peerdev::world_sum, tag arb[s & 1]: mode 3's
+// p-update all-reduce moved one kernel on) — unless rr_held says an
+// end-of-run settle already did. Workgroup 0 records rxr[s] as k_spmv_fd does.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_fd_lean_push(
+    CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
+    T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr, PeerDev P) {
+  __shared__ SellLds<T> sm;
+  __shared__ double wres;
+  __shared__ int wok;
+  const int prev = (slot + 3) & 3;
+  const long long bodies = st->bodies;
+  const bool held = st->rr_held != 0;
+  const bool act = st->active[slot] != 0 && !P.state->fault;
+  if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+  if (!act) {
+    // the first skipped body records the final r.r (every rank skips it)
+    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot && !held &&
+        !P.state->fault) {
+      const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+      const bool ok = peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok);
+      if (threadIdx.x == 0) {
+        if (ok) {
+          st->rr[prev] = (T)wres;
+          st->rxr[slot] = (T)wres;
+          st->rr_held = 1;
+        } else {
+          peerdev::raise_fault(st, slot, P.state);
+        }
+      }
+    }
+    return;
+  }
+  T beta = T(0);
+  if (bodies > 0) {
+    T rr;
+    if (held) {
+      rr = st->rxr[slot];
+    } else {
+      rr = sum_parts(ws->rr_part, np_rr, sm.red);
+      if (!peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok)) {
+        if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
+        return;
+      }
+      rr = (T)wres;
+    }
+    beta = rr / st->rxr[prev];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->rr[prev] = rr;  // the record
+      st->rxr[slot] = rr;
+    }
+  }
+  const GatherP<T> g{r, pold, beta};
+  if ((int)blockIdx.x < A.wg0) {
+    peerdev::push_wg_from<T>(g, P, st, slot, blockIdx.x);
+    return;
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_lean<T>(A, g, e, vd, vt);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+}
+
+// Mode 4 on a partitioned matrix, kernel 2 of 3: the boundary rows as
+// CSR-stream blocks after k_spmv_dot_bnd's wait for the neighbours' pushes;
+// own columns form p_k from r and p_{k-1} with kernel 1's beta (rxr[s] /
+// rxr[s-1]: the same division), ghosts are the pushed p_k in the landing
+// buffer. The rows' p_k and Ap are stored, their p.Ap partials at part_off.
+template <typename T, int V>
+__global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd_bnd(
+    CsrArgs A, const T *__restrict__ val, const T *__restrict__ r, const T *__restrict__ pold,
+    T *__restrict__ pc, T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
+    PeerDev P) {
+  if (peerdev::skip_body(st, slot, P.state)) return;
+  __shared__ int ok_s;
+  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
+  if (threadIdx.x < 64) {
+    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
+    bool ok = true;
+    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
+      ok = ok && peerdev::spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
+                                  P.spin_ticks);
+    ok = __all(ok);
+    if (threadIdx.x == 0) ok_s = ok;
+  }
+  __syncthreads();
+  if (!ok_s) {
+    if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, as k_peer_wait
+  const int prev = (slot + 3) & 3;
+  const T beta = st->bodies > 0 ? st->rxr[slot] / st->rxr[prev] : T(0);
+  __shared__ LdsOf<T, V> sm;
+  const GatherP<T> g{r, pold, beta};
+  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_any<T, V>(A, val, GatherPL<T>{g, reinterpret_cast<const T *>(P.land_local), (int)A.n}, e,
+                 sm);
+  T v[1] = {e.acc};
+  block_sum<T, 1>(v, sm.red);
+  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+}
+
 // The final r.r of a mode-4 run that ended on an active body (no kernel 1
 // followed to record it): rxr[s] of the next slot, as k_spmv_fd records it.
 template <typename T>
@@ -2604,6 +2747,30 @@ __global__ __launch_bounds__(kBlock) void k_rr_settle(CgScalars<T> *st, RedWs<T>
   if (threadIdx.x == 0) {
     st->rr[(slot + 3) & 3] = rr;
     st->rxr[slot] = rr;
+  }
+}
+// ... on a partitioned matrix: the world r.r (the all-reduce the next kernel
+// 1 would run, same tag), held for it (rr_held)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_rr_settle_peer(CgScalars<T> *st, RedWs<T> *ws,
+                                                           int np_rr, PeerDev P) {
+  __shared__ T red[4 * kMaxRed];
+  __shared__ double wres;
+  __shared__ int wok;
+  const long long bodies = st->bodies;
+  if (bodies <= 0 || st->rr_held || P.state->fault) return;
+  const int slot = (int)(bodies & 3);
+  const T rr = sum_parts(ws->rr_part, np_rr, red);
+  const bool ok = peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok);
+  if (threadIdx.x == 0) {
+    if (ok) {
+      st->rr[(slot + 3) & 3] = (T)wres;
+      st->rxr[slot] = (T)wres;
+      st->rr_held = 1;
+    } else {
+      P.state->fault = 1;
+      st->stopped = 3;
+    }
   }
 }
 
@@ -2852,6 +3019,12 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
       st->active[(slot + 1) & 3] = cont ? 1 : 0;
       st->stopped = cond ? 1 : (cont ? 0 : 2);
       st->ran[slot] = 1;
+      if constexpr (PEER) {  // mode 4 partitioned (kernel 3): the next body's tag base
+        const unsigned long long t = P->state->arb[slot & 1] + 2;
+        P->state->ar = t;
+        P->state->arb[(slot + 1) & 1] = t;
+        st->rr_held = 0;
+      }
     }
   }
   T acc = T(0);
@@ -2951,6 +3124,20 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
     update_r_body<T, false, true, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
   else
     update_r_body<T, false, true, false>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
+}
+// Mode 4 on a partitioned matrix, kernel 3 of 3: update_r with the p.Ap
+// all-reduce (tag base + 1), the stop rule and the next body's tag base; in
+// slot 3 (GF) the group's x flush as k_update_r_flush
+template <typename T, bool GF>
+__global__ __launch_bounds__(kBlock) void k_update_r_peer_rule(int64_t n, T *r,
+                                                               const T *__restrict__ Ap,
+                                                               CgScalars<T> *st, int slot,
+                                                               RedWs<T> *ws, int np_pap, int rev,
+                                                               PeerDev P, XFlush<T> xf) {
+  if (stream_nt<T>(n))
+    update_r_body<T, false, true, true, GF>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, &P, &xf);
+  else
+    update_r_body<T, false, true, false, GF>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, &P, &xf);
 }
 
 // x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
@@ -4180,6 +4367,73 @@ hipError_t Launch<T>::update_r_flush(int64_t n, T *r, const T *Ap, CgScalars<T> 
 template <typename T>
 hipError_t Launch<T>::rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s) {
   CGX_LAUNCH(k_rr_settle<T>, 1, st, ws, np_rr);
+}
+template <typename T>
+hipError_t Launch<T>::spmv_fd_lean_push(const CsrDev &A, const T *r, const T *pold, T *pc, T *Ap,
+                                        CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
+                                        hipStream_t s, int rev, const PeerDev &P, int wg0) {
+  if constexpr (!std::is_same<T, double>::value) {
+    return hipErrorInvalidValue;
+  } else {
+    if (!vl_active(A) || !A.vl_split || wg0 < 0 || wg0 % 8) return hipErrorInvalidValue;
+    CsrArgs a = args(A);
+    a.rev = rev;
+    a.part_off = 0;
+    a.wg0 = wg0;
+    CGX_GGL(k_spmv_fd_lean_push<T>, dim3(wg0 + A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
+            Ap, st, slot, ws, np_rr, P);
+    return hipGetLastError();
+  }
+}
+template <typename T>
+hipError_t Launch<T>::spmv_fd_rows_bnd(const CsrDev &A, const int *blocks, int count,
+                                       int part_off, const T *r, const T *pold, T *pc, T *Ap,
+                                       CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s,
+                                       const PeerDev &P) {
+  if constexpr (!std::is_same<T, double>::value) {
+    return hipErrorInvalidValue;
+  } else {
+    const int v = spmv_variant<T>(A, 13);  // 13, or 0 for unaligned val / col
+    if (count < 1 || (v != 13 && v != 0)) return hipErrorInvalidValue;
+    CsrArgs a = args(A);
+    a.rbo = blocks;
+    a.nrb = count;
+    a.part_off = part_off;
+    const T *val = (const T *)A.val;
+    const int grid = rows_grid(A, count);
+    if (v == 13)
+      CGX_GGL((k_spmv_fd_bnd<T, 13>), dim3(grid), dim3(kBlock), 0, s, a, val, r, pold, pc, Ap, st,
+              slot, ws, P);
+    else
+      CGX_GGL((k_spmv_fd_bnd<T, 0>), dim3(grid), dim3(kBlock), 0, s, a, val, r, pold, pc, Ap, st,
+              slot, ws, P);
+    return hipGetLastError();
+  }
+}
+template <typename T>
+hipError_t Launch<T>::update_r_peer_rule(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
+                                         RedWs<T> *ws, int np_pap, int rev, T *x, T *const *P4,
+                                         hipStream_t s, const PeerDev &P) {
+  if constexpr (!std::is_same<T, double>::value) {
+    return hipErrorInvalidValue;
+  } else {
+    const int grid = grid_elems(n, kGridUpdateR);
+    if (P4) {
+      const XFlush<T> xf{x, {P4[0], P4[1], P4[2], P4[3]}};
+      CGX_GGL((k_update_r_peer_rule<T, true>), dim3(grid), dim3(kBlock), 0, s, n, r, Ap, st, slot,
+              ws, np_pap, rev, P, xf);
+    } else {
+      const XFlush<T> xf{nullptr, {nullptr, nullptr, nullptr, nullptr}};
+      CGX_GGL((k_update_r_peer_rule<T, false>), dim3(grid), dim3(kBlock), 0, s, n, r, Ap, st,
+              slot, ws, np_pap, rev, P, xf);
+    }
+    return hipGetLastError();
+  }
+}
+template <typename T>
+hipError_t Launch<T>::rr_settle_peer(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s,
+                                     const PeerDev &P) {
+  CGX_LAUNCH(k_rr_settle_peer<T>, 1, st, ws, np_rr, P);
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
   if (vl_whole(A)) return A.vl_grid;

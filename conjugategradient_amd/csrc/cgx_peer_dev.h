@@ -104,9 +104,11 @@ __device__ __forceinline__ bool world_sum(double mine, unsigned long long t, con
 // releases them at system scope and raises the flag (MI355X guide, "Valid
 // forms"; the asm wait after the fence guards the compiler hazard noted
 // there).
-template <typename T>
-__device__ __forceinline__ void push_wg(const T *__restrict__ v, const PeerDev &P,
-                                        CgScalars<T> *st, int slot, int wg) {
+// get(j): the value pushed for own row j (v[j], or mode 4's p_k formed as
+// r_j + beta p_{k-1,j}: the value the owner's SpMV forms for its own rows)
+template <typename T, class Get>
+__device__ __forceinline__ void push_wg_from(const Get &get, const PeerDev &P, CgScalars<T> *st,
+                                             int slot, int wg) {
   if (skip_body(st, slot, P.state)) return;
   const unsigned long long tag = body_tag(st, slot, P.state);
   const int i = wg / kPushWG, g = wg % kPushWG;
@@ -114,7 +116,7 @@ __device__ __forceinline__ void push_wg(const T *__restrict__ v, const PeerDev &
   const int64_t c0 = cnt * g / kPushWG, c1 = cnt * (g + 1) / kPushWG;
   T *dst = reinterpret_cast<T *>(P.land_remote[i]);
   const int *idx = P.send_idx + off;
-  for (int64_t k = c0 + threadIdx.x; k < c1; k += kBlock) dst[k] = v[idx[k]];
+  for (int64_t k = c0 + threadIdx.x; k < c1; k += kBlock) dst[k] = get(idx[k]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -123,6 +125,11 @@ __device__ __forceinline__ void push_wg(const T *__restrict__ v, const PeerDev &
     auto *flag = reinterpret_cast<unsigned long long *>(P.ctl[P.send_rank[i]] + kPeerFlagOff);
     st_sys(flag + P.rank * kPushWG + g, tag);
   }
+}
+template <typename T>
+__device__ __forceinline__ void push_wg(const T *__restrict__ v, const PeerDev &P,
+                                        CgScalars<T> *st, int slot, int wg) {
+  push_wg_from<T>([v](int j) { return v[j]; }, P, st, slot, wg);
 }
 
 template <typename T>

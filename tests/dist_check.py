@@ -48,7 +48,10 @@ def main():
                          "iteration (cgx_dist_peer_enable; must pass its self-test); "
                          "'host-async': the host exchange on the comm stream, overlapped "
                          "with the interior slices (cgx_dist_host_async)")
-    ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3)")
+    ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3, 4)")
+    ap.add_argument("--runs", type=int, default=1,
+                    help="split the solve into this many cgx_cg_run calls after one "
+                         "cgx_cg_begin (each run ends with its end-of-run flush)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -110,7 +113,16 @@ def main():
     check(L.cgx_cg_set_mode(cg, a.mode))
     bodies, rxr = C.c_int64(), C.c_double()
     tol = 0.0 if a.bodies >= 0 else a.tol
-    check(L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, a.bodies, C.byref(bodies), C.byref(rxr)))
+    if a.runs > 1:
+        check(L.cgx_cg_begin(cg, b.ptr, x.ptr, tol, a.bodies))
+        per = max(1, (a.bodies if a.bodies >= 0 else 120) // a.runs)
+        stopped = C.c_int(0)
+        while not stopped.value:
+            check(L.cgx_cg_run(cg, per, C.byref(bodies), C.byref(stopped)))
+    else:
+        check(L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, a.bodies, C.byref(bodies), C.byref(rxr)))
+    mode_run = C.c_int()
+    check(L.cgx_cg_get_mode(cg, C.byref(mode_run)))
     acalls = C.c_int64()
     check(L.cgx_csr_halo_async_calls(A, C.byref(acalls)))
     acc = C.c_double()
@@ -144,6 +156,7 @@ def main():
         ok = bool(relerr <= 1e-10 and abs(bodies.value - oracle_bodies) <= 2
                   and np.isfinite(xg).all())
         print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode,
+                          "mode_run": mode_run.value, "runs": a.runs,
                           "grid": [gxy, gxy, g], "bodies": bodies.value,
                           "oracle_bodies": oracle_bodies, "rel_err": relerr,
                           "accuracy": acc.value, "ghosts": [p[0] for p in parts],

@@ -107,6 +107,47 @@ def test_partitioned_lean_interior(nproc, transport):
     assert all(ni > 0 and nb > 0 for ni, nb in r["split"]), r["split"]
 
 
+LEAN = {"CGX_SPMV_VARIANT": "33554432:0"}
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_partitioned_mode4_bit_identical_to_mode3(nproc):
+    """Mode 4 on the partitioned body (round 5): kernel 1 walks the interior
+    forming p_k = r + beta p_{k-1} and pushes the formed p_k of the send rows
+    from its first workgroups (beta from the WORLD r.r, all-reduced there),
+    kernel 2 runs the boundary rows after the neighbours' pushes, kernel 3 is
+    update_r with the p.Ap all-reduce, the stop rule and the slot-3 x flush.
+    Its SpMV partials split as mode 3's (the walk's grid, the boundary row
+    blocks' grid) and every formed value is mode 3's p update, so x is bit
+    for bit mode 3's; 30 bodies at tol 0 against the oracle (rel 1e-10)."""
+    args = ["--nxy", "128", "--bodies", "30"]
+    r4 = _run(nproc, "host-peer", 48, 4, args, env=LEAN)
+    r3 = _run(nproc, "host-peer", 48, 3, args, env=LEAN)
+    assert r4["ok"] and r3["ok"], (r4, r3)
+    assert r4["mode_run"] == 4 and r3["mode_run"] == 3
+    assert r4["bodies"] == r3["bodies"] == 30
+    for var, _ in r4["variant_lean_slices"]:
+        assert var & 33554432, r4["variant_lean_slices"]
+    assert r4["x_sha"] == r3["x_sha"], (r4, r3)
+
+
+def test_partitioned_mode4_stop_rule_and_resumed_runs():
+    """The stop rule and the run boundaries of partitioned mode 4: solved to
+    tolerance (the first skipped body records the final world r.r), and the
+    same solve split into cgx_cg_run calls of 40 bodies (each run's end
+    settles the world r.r with k_rr_settle_peer and holds it for the next
+    run's kernel 1, rr_held). Both end on the oracle's body count (+-2) and
+    x (rel 1e-10), bit-identical to each other and to mode 3."""
+    args = ["--nxy", "128"]
+    r1 = _run(2, "host-peer", 48, 4, args, env=LEAN)
+    rr = _run(2, "host-peer", 48, 4, args + ["--runs", "3"], env=LEAN)
+    r3 = _run(2, "host-peer", 48, 3, args, env=LEAN)
+    assert r1["ok"] and rr["ok"] and r3["ok"], (r1, rr, r3)
+    assert r1["mode_run"] == rr["mode_run"] == 4
+    assert r1["bodies"] == rr["bodies"] == r3["bodies"]
+    assert r1["x_sha"] == rr["x_sha"] == r3["x_sha"], (r1, rr, r3)
+
+
 def test_partitioned_ranks_share_the_sellp_layout():
     """Without forcing a form, the ranks above rank 0 (whose boundary rows
     gather ghosts numbered after their own rows) get the SELL-P value-code
