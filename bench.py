@@ -484,6 +484,18 @@ def run(args) -> None:
     fused = args.mode == 2
     me = C.c_int(0)
     check(L.cgx_cg_get_mode(cg, C.byref(me)))
+    if dist_on and world > 1 and me.value == 4 and args.mode == 0:
+        # the auto partitioned mode 4 runs its own kernels over the peer
+        # transport: validated as the transport was (a 128 x 128 slab per rank,
+        # against the setup transport's solve), else the body stays mode 3
+        v4 = validate_peer(L, q, world, rank, dist, nxy=128, mode=4)
+        if validation is not None:
+            validation["mode4"] = v4
+        if not v4["ok"]:
+            check(L.cgx_cg_set_mode(cg, 3))
+            check(L.cgx_cg_get_mode(cg, C.byref(me)))
+            peer_note = (peer_note or "") + f" partitioned mode 4 failed its validation " \
+                                            f"({v4.get('why')}): mode 3"
     if dist_on and me.value == 4:
         sfx = "_push"  # partitioned mode 4: the interior walk with the push in front
     mode_eff = me.value
@@ -792,14 +804,15 @@ def pmc_traffic(args, variant: str, mode: int, team: int = 0, timeout_s: float =
                       "correction, MI355X_MICROARCH.md)"}
 
 
-def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
+def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8, mode=0):
     """Solve a small slab problem (nxy x nxy x planes*world, `planes` z-planes
     per rank, b_i = i + 1, x0 = 0) twice on this node: over the device peer
     transport and over the context's setup transport (RCCL; the host
     transport in the one-GPU rehearsal). The peer transport passes when both solves
     converge (accuracy() < 1e-20), their body counts agree within 2, and
     their x agree to 1e-10 relative (SURVEY §8(c) tolerances). Collective;
-    every rank returns the same verdict."""
+    every rank returns the same verdict. mode 4: the peer solve runs the
+    partitioned mode 4 (its kernels, with the lean interior walk forced)."""
     import numpy as np
     import torch
 
@@ -836,9 +849,15 @@ def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
             x = cga.DeviceArray(q, n_local, np.float64)
             x.fill(0.0)
             cg = C.c_void_p()
+            rc = 0
+            if name == "peer" and mode == 4:
+                rc = L.cgx_csr_set_variant(A, KVL)
             check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
+            if rc == 0 and name == "peer" and mode == 4:
+                rc = L.cgx_cg_set_mode(cg, 4)
             bodies, rxr, acc = C.c_int64(), C.c_double(), C.c_double()
-            rc = L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, -1, C.byref(bodies), C.byref(rxr))
+            if rc == 0:
+                rc = L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, -1, C.byref(bodies), C.byref(rxr))
             if rc == 0:
                 check(L.cgx_accuracy(q.handle, A, b.ptr, x.ptr, C.byref(acc)))
                 xs[name] = x.download()
@@ -871,7 +890,7 @@ def validate_peer(L, q, world, rank, dist, nxy=48, planes=8, tol=1e-8):
     if not ok and why is None:
         why = "another rank's validation failed"
     return {"ok": bool(ok), "grid": [nxy, nxy, nz], "tol": tol, "solves": out,
-            "x_rel_peer_vs_setup": rel, "why": why}
+            "x_rel_peer_vs_setup": rel, "why": why, "peer_mode": mode or "auto"}
 
 
 def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):

@@ -97,14 +97,18 @@ struct StateView {
   int stopped;
   double rxr;
 };
+// (tail_fault: partitioned mode 4's last-workgroup r.r all-reduce timed out —
+// the run stops as on stopped == 3)
 StateView view_state(const cgx_cg *cg, const void *h, int slot) {
   StateView v{};
   if (cg->dtype == CGX_F32) {
     const auto *s = (const CgScalars<float> *)h;
-    v = StateView{s->active[slot], s->bodies, s->stopped, (double)s->rxr[slot]};
+    v = StateView{s->tail_fault ? 0 : s->active[slot], s->bodies,
+                  s->tail_fault ? 3 : s->stopped, (double)s->rxr[slot]};
   } else {
     const auto *s = (const CgScalars<double> *)h;
-    v = StateView{s->active[slot], s->bodies, s->stopped, s->rxr[slot]};
+    v = StateView{s->tail_fault ? 0 : s->active[slot], s->bodies,
+                  s->tail_fault ? 3 : s->stopped, s->rxr[slot]};
   }
   return v;
 }
@@ -403,7 +407,7 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
     const int gi = A->dev.vl_grid;
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = Launch<T>::spmv_fd_lean_push(A->dev, r, P[(slot + 3) & 3], P[slot], Ap,
-                                                       st, slot, ws, npr, s, par, PD, wg0);
+                                                       st, slot, ws, s, par, PD, wg0);
            if (e == hipSuccess)
              e = Launch<T>::spmv_fd_rows_bnd(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, r,
                                              P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, s, PD);
@@ -509,11 +513,8 @@ int flush_pending_x(cgx_cg *cg) {
       if (cg->slot != 0)
         CGX_HIP(Launch<double>::flush_defer(cg->n, (double *)cg->x, P,
                                             (CgScalars<double> *)cg->st, s));
-      if (cg->A->dist)  // the world r.r (dist_fd_ok: the device peer transport)
-        CGX_HIP(Launch<double>::rr_settle_peer((CgScalars<double> *)cg->st,
-                                               (RedWs<double> *)cg->ws, npr, s,
-                                               cg->A->peer.dev));
-      else
+      // (partitioned: kernel 3 recorded the world r.r itself)
+      if (!cg->A->dist)
         CGX_HIP(Launch<double>::rr_settle((CgScalars<double> *)cg->st, (RedWs<double> *)cg->ws,
                                           npr, s));
     }

@@ -37,11 +37,10 @@ template <typename T> struct CgScalars {
   int stopped;       // 0 running, 1 stop rule (tol / NaN), 2 cap reached,
                      // 3 peer transport fault (a spin timed out), 4 a mode-5
                      // grid-wide exchange timed out
-  // mode 4 on a partitioned matrix: rxr[bodies & 3] already holds the world
-  // r.r of the last body (an end-of-run k_rr_settle_peer or the first skipped
-  // body recorded it), so the next kernel 1 takes it instead of all-reducing
-  // the partials again (their tag may be spent). Cleared by kernel 2.
-  int rr_held;
+  // mode 4 on a partitioned matrix: the r.r all-reduce in kernel 3's last
+  // workgroup timed out (written by that workgroup only: stopped and active
+  // belong to workgroup 0 of the same launch); the host stops as on 3
+  int tail_fault;
   // deferred x update (mode 3, cgx_abi.cpp enqueue_iter_defer): alpha of the
   // body in slot s, set by its update_r; ran[s]: the body ran and its x
   // update is not applied yet (set by its update_xp, cleared by the slot-3
@@ -298,19 +297,17 @@ template <typename T> struct Launch {
   // with CSR-stream boundary rows), f64: kernel 1 (interior walk forming p_k,
   // the formed p_k pushed by the first wg0 workgroups; partials [0, vl_grid)),
   // kernel 2 (boundary row blocks, partials from part_off), kernel 3
-  // (update_r with the stop rule; P non-null in slot 3: the group flush),
-  // and the end-of-run world r.r
+  // (update_r with the stop rule and the world r.r; P4 non-null in slot 3:
+  // the group flush)
   static hipError_t spmv_fd_lean_push(const CsrDev &A, const T *r, const T *pold, T *pc, T *Ap,
-                                      CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
-                                      hipStream_t s, int rev, const PeerDev &P, int wg0);
+                                      CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s,
+                                      int rev, const PeerDev &P, int wg0);
   static hipError_t spmv_fd_rows_bnd(const CsrDev &A, const int *blocks, int count, int part_off,
                                      const T *r, const T *pold, T *pc, T *Ap, CgScalars<T> *st,
                                      int slot, RedWs<T> *ws, hipStream_t s, const PeerDev &P);
   static hipError_t update_r_peer_rule(int64_t n, T *r, const T *Ap, CgScalars<T> *st, int slot,
                                        RedWs<T> *ws, int np_pap, int rev, T *x,
                                        T *const *P4, hipStream_t s, const PeerDev &P);
-  static hipError_t rr_settle_peer(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s,
-                                   const PeerDev &P);
   // partial counts the consumers pass (the producers' grid sizes)
   static int spmv_parts(const CsrDev &A);
   // SpMV + p.Ap over `count` SELL slices listed at `list` (device), partials

@@ -2317,7 +2317,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
     st->bodies = 0;
     st->cap = cap;
     st->stopped = 0;
-    st->rr_held = 0;
+    st->tail_fault = 0;
   }
 }
 
@@ -2622,60 +2622,22 @@ __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
 // Mode 4 on a partitioned matrix (device peer transport), kernel 1 of 3:
 // k_spmv_fd_lean over the interior slices, with the halo push of the formed
 // p_k (the value this rank's own SpMV forms for those rows) in the first
-// A.wg0 workgroups. beta needs the WORLD r.r of body k-1, so every workgroup
-// all-reduces the partials here (peerdev::world_sum, tag arb[s & 1]: mode 3's
-// p-update all-reduce moved one kernel on) — unless rr_held says an
-// end-of-run settle already did. Workgroup 0 records rxr[s] as k_spmv_fd does.
+// A.wg0 workgroups. beta = rxr[s] / rxr[s-1]: the world r.r of body k-1 was
+// all-reduced by the last workgroup of its kernel 3 (k_update_r_peer_rule),
+// so no workgroup here waits on another rank (on a GPU shared by ranks, a
+// whole grid spinning would hold the CUs the other ranks need to publish).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean_push(
     CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
-    T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr, PeerDev P) {
+    T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, PeerDev P) {
   __shared__ SellLds<T> sm;
-  __shared__ double wres;
-  __shared__ int wok;
   const int prev = (slot + 3) & 3;
   const long long bodies = st->bodies;
-  const bool held = st->rr_held != 0;
   const bool act = st->active[slot] != 0 && !P.state->fault;
   if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
     for (int t = 0; t < 4; ++t) st->ran[t] = 0;
-  if (!act) {
-    // the first skipped body records the final r.r (every rank skips it)
-    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot && !held &&
-        !P.state->fault) {
-      const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
-      const bool ok = peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok);
-      if (threadIdx.x == 0) {
-        if (ok) {
-          st->rr[prev] = (T)wres;
-          st->rxr[slot] = (T)wres;
-          st->rr_held = 1;
-        } else {
-          peerdev::raise_fault(st, slot, P.state);
-        }
-      }
-    }
-    return;
-  }
-  T beta = T(0);
-  if (bodies > 0) {
-    T rr;
-    if (held) {
-      rr = st->rxr[slot];
-    } else {
-      rr = sum_parts(ws->rr_part, np_rr, sm.red);
-      if (!peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok)) {
-        if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
-        return;
-      }
-      rr = (T)wres;
-    }
-    beta = rr / st->rxr[prev];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->rr[prev] = rr;  // the record
-      st->rxr[slot] = rr;
-    }
-  }
+  if (!act) return;
+  const T beta = bodies > 0 ? st->rxr[slot] / st->rxr[prev] : T(0);
   const GatherP<T> g{r, pold, beta};
   if ((int)blockIdx.x < A.wg0) {
     peerdev::push_wg_from<T>(g, P, st, slot, blockIdx.x);
@@ -2697,9 +2659,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean_push(
 
 // Mode 4 on a partitioned matrix, kernel 2 of 3: the boundary rows as
 // CSR-stream blocks after k_spmv_dot_bnd's wait for the neighbours' pushes;
-// own columns form p_k from r and p_{k-1} with kernel 1's beta (rxr[s] /
-// rxr[s-1]: the same division), ghosts are the pushed p_k in the landing
-// buffer. The rows' p_k and Ap are stored, their p.Ap partials at part_off.
+// own columns form p_k from r and p_{k-1} with kernel 1's beta (the same
+// division), ghosts are the pushed p_k in the landing buffer. The rows' p_k
+// and Ap are stored, their p.Ap partials at part_off.
 template <typename T, int V>
 __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd_bnd(
     CsrArgs A, const T *__restrict__ val, const T *__restrict__ r, const T *__restrict__ pold,
@@ -2747,30 +2709,6 @@ __global__ __launch_bounds__(kBlock) void k_rr_settle(CgScalars<T> *st, RedWs<T>
   if (threadIdx.x == 0) {
     st->rr[(slot + 3) & 3] = rr;
     st->rxr[slot] = rr;
-  }
-}
-// ... on a partitioned matrix: the world r.r (the all-reduce the next kernel
-// 1 would run, same tag), held for it (rr_held)
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_rr_settle_peer(CgScalars<T> *st, RedWs<T> *ws,
-                                                           int np_rr, PeerDev P) {
-  __shared__ T red[4 * kMaxRed];
-  __shared__ double wres;
-  __shared__ int wok;
-  const long long bodies = st->bodies;
-  if (bodies <= 0 || st->rr_held || P.state->fault) return;
-  const int slot = (int)(bodies & 3);
-  const T rr = sum_parts(ws->rr_part, np_rr, red);
-  const bool ok = peerdev::world_sum((double)rr, P.state->arb[slot & 1], P, &wres, &wok);
-  if (threadIdx.x == 0) {
-    if (ok) {
-      st->rr[(slot + 3) & 3] = (T)wres;
-      st->rxr[slot] = (T)wres;
-      st->rr_held = 1;
-    } else {
-      P.state->fault = 1;
-      st->stopped = 3;
-    }
   }
 }
 
@@ -3019,12 +2957,6 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
       st->active[(slot + 1) & 3] = cont ? 1 : 0;
       st->stopped = cond ? 1 : (cont ? 0 : 2);
       st->ran[slot] = 1;
-      if constexpr (PEER) {  // mode 4 partitioned (kernel 3): the next body's tag base
-        const unsigned long long t = P->state->arb[slot & 1] + 2;
-        P->state->ar = t;
-        P->state->arb[(slot + 1) & 1] = t;
-        st->rr_held = 0;
-      }
     }
   }
   T acc = T(0);
@@ -3067,7 +2999,12 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   T v[1] = {acc};
   if constexpr (!FUSED) {  // this workgroup's share of r.r; the next kernel sums them
     block_sum<T, 1>(v, red);
-    if (threadIdx.x == 0) ws->rr_part[blockIdx.x] = v[0];
+    if (threadIdx.x == 0) {
+      if (PEER && rule)  // ... or this kernel's last workgroup (k_update_r_peer_rule)
+        store_sc1(&ws->rr_part[blockIdx.x], v[0]);
+      else
+        ws->rr_part[blockIdx.x] = v[0];
+    }
     return;
   }
   if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) {
@@ -3125,9 +3062,36 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
   else
     update_r_body<T, false, true, false>(n, r, r, Ap, st, slot, ws, np_pap, rev, 0, &P);
 }
+// true in the workgroup of the grid that arrives last (two-level tickets as
+// grid_reduce: ticket[b % kRedGroups], then top; each reset by its last
+// arrival). Thread 0 of every workgroup has issued its sc1 stores before.
+template <typename T> __device__ __forceinline__ bool last_arrival(RedWs<T> *ws, int *flag) {
+  const unsigned G = gridDim.x, g = blockIdx.x % kRedGroups;
+  const unsigned ngroups = G < (unsigned)kRedGroups ? G : (unsigned)kRedGroups;
+  const unsigned members = (G - g + kRedGroups - 1) / kRedGroups;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool last = __hip_atomic_fetch_add(&ws->ticket[g], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) == members - 1;
+    if (last) {
+      __hip_atomic_store(&ws->ticket[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(&ws->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             ngroups - 1;
+      if (last) __hip_atomic_store(&ws->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 // Mode 4 on a partitioned matrix, kernel 3 of 3: update_r with the p.Ap
-// all-reduce (tag base + 1), the stop rule and the next body's tag base; in
-// slot 3 (GF) the group's x flush as k_update_r_flush
+// all-reduce (tag base + 1) and the stop rule; in slot 3 (GF) the group's x
+// flush as k_update_r_flush. The workgroup that finishes last sums the r.r
+// partials (sum_parts order over sc1 loads: mode 3's value) and all-reduces
+// them (tag base + 2, as mode 3's p update), records the world r.r where the
+// next body's kernels 1 and 2 read it (rxr[s+1]) and sets the next body's
+// tag base: one workgroup waits on the other ranks, not a whole grid.
 template <typename T, bool GF>
 __global__ __launch_bounds__(kBlock) void k_update_r_peer_rule(int64_t n, T *r,
                                                                const T *__restrict__ Ap,
@@ -3138,6 +3102,34 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer_rule(int64_t n, T *r,
     update_r_body<T, false, true, true, GF>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, &P, &xf);
   else
     update_r_body<T, false, true, false, GF>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, &P, &xf);
+  // every workgroup arrives, whichever way it left the body (a ticket left
+  // short would break the next grid reduction on this workspace)
+  __shared__ int lastf;
+  if (!last_arrival(ws, &lastf)) return;
+  if (!st->active[slot] || P.state->fault) return;
+  __shared__ T red[4];
+  __shared__ T bc;
+  T v[1] = {T(0)};
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += kBlock) v[0] += load_sc1(&ws->rr_part[i]);
+  block_sum<T, 1>(v, red);
+  if (threadIdx.x == 0) bc = v[0];
+  __syncthreads();
+  const unsigned long long t = P.state->arb[slot & 1] + 2;
+  __shared__ double wres;
+  __shared__ int wok;
+  const bool ok = peerdev::world_sum((double)bc, t, P, &wres, &wok);
+  if (threadIdx.x == 0) {
+    if (!ok) {
+      P.state->fault = 1;
+      st->tail_fault = 1;
+      return;
+    }
+    const T w = (T)wres;
+    st->rr[slot] = w;  // the record
+    st->rxr[(slot + 1) & 3] = w;
+    P.state->ar = t;
+    P.state->arb[(slot + 1) & 1] = t;
+  }
 }
 
 // x = x + alpha p ; p = r + beta p ; stop rule   (CG.hpp:390, 396-418, 436)
@@ -4370,8 +4362,8 @@ hipError_t Launch<T>::rr_settle(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipSt
 }
 template <typename T>
 hipError_t Launch<T>::spmv_fd_lean_push(const CsrDev &A, const T *r, const T *pold, T *pc, T *Ap,
-                                        CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
-                                        hipStream_t s, int rev, const PeerDev &P, int wg0) {
+                                        CgScalars<T> *st, int slot, RedWs<T> *ws, hipStream_t s,
+                                        int rev, const PeerDev &P, int wg0) {
   if constexpr (!std::is_same<T, double>::value) {
     return hipErrorInvalidValue;
   } else {
@@ -4381,7 +4373,7 @@ hipError_t Launch<T>::spmv_fd_lean_push(const CsrDev &A, const T *r, const T *po
     a.part_off = 0;
     a.wg0 = wg0;
     CGX_GGL(k_spmv_fd_lean_push<T>, dim3(wg0 + A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc,
-            Ap, st, slot, ws, np_rr, P);
+            Ap, st, slot, ws, P);
     return hipGetLastError();
   }
 }
@@ -4429,11 +4421,6 @@ hipError_t Launch<T>::update_r_peer_rule(int64_t n, T *r, const T *Ap, CgScalars
     }
     return hipGetLastError();
   }
-}
-template <typename T>
-hipError_t Launch<T>::rr_settle_peer(CgScalars<T> *st, RedWs<T> *ws, int np_rr, hipStream_t s,
-                                     const PeerDev &P) {
-  CGX_LAUNCH(k_rr_settle_peer<T>, 1, st, ws, np_rr, P);
 }
 template <typename T> int Launch<T>::spmv_parts(const CsrDev &A) {
   if (vl_whole(A)) return A.vl_grid;

@@ -114,9 +114,9 @@ LEAN = {"CGX_SPMV_VARIANT": "33554432:0"}
 def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     """Mode 4 on the partitioned body (round 5): kernel 1 walks the interior
     forming p_k = r + beta p_{k-1} and pushes the formed p_k of the send rows
-    from its first workgroups (beta from the WORLD r.r, all-reduced there),
-    kernel 2 runs the boundary rows after the neighbours' pushes, kernel 3 is
-    update_r with the p.Ap all-reduce, the stop rule and the slot-3 x flush.
+    from its first workgroups, kernel 2 runs the boundary rows after the
+    neighbours' pushes, kernel 3 is update_r with the p.Ap all-reduce, the
+    stop rule and the slot-3 x flush, its last workgroup all-reducing r.r.
     Its SpMV partials split as mode 3's (the walk's grid, the boundary row
     blocks' grid) and every formed value is mode 3's p update, so x is bit
     for bit mode 3's; 30 bodies at tol 0 against the oracle (rel 1e-10)."""
@@ -133,11 +133,11 @@ def test_partitioned_mode4_bit_identical_to_mode3(nproc):
 
 def test_partitioned_mode4_stop_rule_and_resumed_runs():
     """The stop rule and the run boundaries of partitioned mode 4: solved to
-    tolerance (the first skipped body records the final world r.r), and the
-    same solve split into cgx_cg_run calls of 40 bodies (each run's end
-    settles the world r.r with k_rr_settle_peer and holds it for the next
-    run's kernel 1, rr_held). Both end on the oracle's body count (+-2) and
-    x (rel 1e-10), bit-identical to each other and to mode 3."""
+    tolerance, and the same solve split into cgx_cg_run calls of 40 bodies
+    (each run ends with its x flush; kernel 3's last workgroup has already
+    recorded the world r.r the next run's kernel 1 forms beta from). Both
+    end on the oracle's body count (+-2) and x (rel 1e-10), bit-identical to
+    each other and to mode 3."""
     args = ["--nxy", "128"]
     r1 = _run(2, "host-peer", 48, 4, args, env=LEAN)
     rr = _run(2, "host-peer", 48, 4, args + ["--runs", "3"], env=LEAN)

@@ -69,14 +69,20 @@ def main():
     check(L.cgx_csr_variant(A, C.byref(var)))
     b = cga.DeviceArray(q, nl, np.float64)
     check(L.cgx_iota(q.handle, F64, b.ptr, nl, float(begin)))
-    out = {"world": world, "slab": [nxy, nxy, a.planes], "variant": var.value, "modes": {}}
+    from bench import autotune_record
+    out = {"world": world, "slab": [nxy, nxy, a.planes], "variant": var.value,
+           "forced": os.environ.get("CGX_SPMV_VARIANT"), "autotune": autotune_record(L, A),
+           "modes": {}}
     for mode in [int(m) for m in a.modes.split(",")]:
         x = cga.DeviceArray(q, nl, np.float64)
         x.fill(0.0)
         cg = C.c_void_p()
         check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
         check(L.cgx_cg_config(cg, 64, 1))
-        check(L.cgx_cg_set_mode(cg, mode))
+        if L.cgx_cg_set_mode(cg, mode) != 0:
+            out["modes"][str(mode)] = {"error": L.cgx_last_error().decode()}
+            L.cgx_cg_destroy(cg)
+            continue
         total = a.warmup + a.steps + a.profile
         check(L.cgx_cg_begin(cg, b.ptr, x.ptr, 0.0, total + 1))
         bodies, stopped = C.c_int64(), C.c_int()
