@@ -134,6 +134,7 @@ def parse(argv=None):
     ap.add_argument("--lean-team", choices=["auto", "0", "1"], default="auto",
                     help=argparse.SUPPRESS)  # A/B: the lean walk's team form off / on
     ap.add_argument("--master-port", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--force-lean", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -436,6 +437,8 @@ def run(args) -> None:
                                wl.vals.ptr, F64, None, C.byref(A)))
     if args.lean_team != "auto" and not dist_on:  # A/B of the lean walk's team form
         check(L.cgx_csr_set_lean_team(A, int(args.lean_team)))
+    if args.force_lean:  # the lean walk whatever the autotune chose (tests)
+        check(L.cgx_csr_set_variant(A, KVL))
     peer_note = None
     validation = None
     use_peer = world > 1 and args.transport in ("peer", "host-peer")
@@ -484,18 +487,25 @@ def run(args) -> None:
     fused = args.mode == 2
     me = C.c_int(0)
     check(L.cgx_cg_get_mode(cg, C.byref(me)))
-    if dist_on and world > 1 and me.value == 4 and args.mode == 0:
-        # the auto partitioned mode 4 runs its own kernels over the peer
-        # transport: validated as the transport was (a 128 x 128 slab per rank,
-        # against the setup transport's solve), else the body stays mode 3
-        v4 = validate_peer(L, q, world, rank, dist, nxy=128, mode=4)
-        if validation is not None:
-            validation["mode4"] = v4
-        if not v4["ok"]:
+    if dist_on and world > 1 and args.mode == 0:
+        # the ranks agree on the body: each rank's autotune picks its own
+        # interior form and auto mode 4 needs the lean one, so mode 4 runs only
+        # where every rank took it, and only after it solved a 128 x 128 slab
+        # per rank over the peer transport to the setup transport's answer
+        import torch
+        t4 = torch.tensor([1.0 if me.value == 4 else 0.0], dtype=torch.float64)
+        dist.all_reduce(t4, op=dist.ReduceOp.MIN)
+        why4 = None if t4.item() == 1.0 else "not every rank's interior takes it"
+        if why4 is None:
+            v4 = validate_peer(L, q, world, rank, dist, nxy=128, mode=4)
+            if validation is not None:
+                validation["mode4"] = v4
+            if not v4["ok"]:
+                why4 = f"failed its validation ({v4.get('why')})"
+        if why4 is not None and me.value == 4:
             check(L.cgx_cg_set_mode(cg, 3))
             check(L.cgx_cg_get_mode(cg, C.byref(me)))
-            peer_note = (peer_note or "") + f" partitioned mode 4 failed its validation " \
-                                            f"({v4.get('why')}): mode 3"
+            peer_note = (peer_note or "") + f" partitioned mode 4 {why4}: mode 3"
     if dist_on and me.value == 4:
         sfx = "_push"  # partitioned mode 4: the interior walk with the push in front
     mode_eff = me.value
@@ -665,8 +675,12 @@ def run(args) -> None:
                        "transport_validation": validation,
                        "iteration": {1: "3 kernels", 2: "fused (2 kernels)",
                                      3: "3 kernels, x update deferred over 4 bodies",
-                                     4: "2 kernels (p update in the SpMV), x update deferred "
-                                        "over 4 bodies",
+                                     4: ("3 launches (interior walk forming p_k with the halo "
+                                         "push in front, boundary rows, update_r with both "
+                                         "all-reduces), x update deferred over 4 bodies"
+                                         if dist_on and world > 1 else
+                                         "2 kernels (p update in the SpMV), x update deferred "
+                                         "over 4 bodies"),
                                      5: "persistent body (one launch per chunk of bodies, two "
                                         "grid-wide exchanges per body)"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),

@@ -2730,7 +2730,15 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
 // 512^3 405 against 467, the G3 stand-in (CSR-stream) 19.96k against 22.5k.
 static bool fd_auto(const cgx_cg *cg) {
   const cgx_csr *A = cg->A;
-  if (A->dist || cg->dtype != CGX_F64 || !Launch<double>::fd_supported(A->dev)) return false;
+  // partitioned: the lean interior with this rank's vectors inside the
+  // Infinity Cache (<= 4 M rows, lean_cached's bound below): on the 2-rank
+  // rehearsal of 256^3 / 8's 256 x 256 x 32 slab 95.3-96.3 us per body
+  // against 101.5-102.8 in mode 3 (profiles/r05u_dist_rehearsal.log). A
+  // partitioned body uses the same push, wait and all-reduce tags in modes 3
+  // and 4, so a rank whose autotune gave it another interior form can run
+  // mode 3 beside them (bench.py still makes the ranks agree)
+  if (A->dist) return dist_fd_ok(A, cg->dtype) && A->dev.n <= (int64_t(4) << 20);
+  if (cg->dtype != CGX_F64 || !Launch<double>::fd_supported(A->dev)) return false;
   const int v = launch_variant(A->dev, cg->dtype);
   const bool march2d = (v & 2097152) && A->dev.march_a == 0;
   const bool small = A->dev.nnz * (int64_t)(sizeof(double) + sizeof(int)) < (int64_t(64) << 20);

@@ -214,6 +214,29 @@ def test_bench_two_ranks_autotune_takes_the_lean_interior():
             assert f["how"] == "k_spmv_dot (interior slices)", f
 
 
+def test_bench_four_ranks_auto_mode4_validated():
+    """128^3 over 4 ranks (128 x 128 x 32 slabs, inside the auto rule's 4 M
+    rows) with the lean interior on every rank: bench.py's auto mode takes the
+    partitioned mode 4 only after every rank agreed and it solved a 128 x 128
+    slab problem over the peer transport to the setup transport's answer
+    (config.transport_validation.mode4), then times it. (256^3 over 4 ranks
+    sharing this one GPU times out in mode 3 as in mode 4: each rank's
+    boundary launch waits for pushes with its whole grid resident, and four
+    such grids hold the CUs a late rank needs for its push —
+    gpurun_out/r5w, round 5; one rank per GPU has no such contention.)"""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--grid", "128",
+           "--steps", "20", "--warmup", "5", "--transport", "host-peer", "--no-cpu",
+           "--profile-steps", "0", "--force-lean", "--master-port", str(_port())]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = line["config"]
+    v4 = cfg["transport_validation"]["mode4"]
+    assert v4["ok"] and v4["peer_mode"] == 4, v4
+    assert cfg["iteration"].startswith("3 launches (interior walk forming p_k"), cfg["iteration"]
+    assert cfg["peer_fallback_reason"] is None, cfg["peer_fallback_reason"]
+
+
 def test_bench_rccl_iteration_at_world_size_one():
     """--transport rccl at N = 1: the partitioned path over a one-rank RCCL
     communicator (the all-reduces run, no halo), timed as the line's value

@@ -79,8 +79,13 @@ def main():
         cg = C.c_void_p()
         check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
         check(L.cgx_cg_config(cg, 64, 1))
-        if L.cgx_cg_set_mode(cg, mode) != 0:
-            out["modes"][str(mode)] = {"error": L.cgx_last_error().decode()}
+        # every rank runs the mode or none does (the autotune may give the
+        # ranks different forms, and mode 4 needs the lean interior)
+        rc = L.cgx_cg_set_mode(cg, mode)
+        errs = [None] * world
+        dist.all_gather_object(errs, L.cgx_last_error().decode() if rc else None)
+        if any(errs):
+            out["modes"][str(mode)] = {"error": [e for e in errs]}
             L.cgx_cg_destroy(cg)
             continue
         total = a.warmup + a.steps + a.profile
