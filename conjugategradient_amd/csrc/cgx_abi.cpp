@@ -378,7 +378,7 @@ bool dist_fd_ok(const cgx_csr *A, int dtype) {
          A->dev.vl_split && A->bnd_nblk > 0;
 }
 
-// Fused deferred-x iteration (mode 4, single device): two kernels per body.
+// Fused deferred-x iteration (mode 4): two kernels per body on one device.
 // Kernel 1 computes p_k = r + beta p_{k-1} where the SpMV reads it and
 // stores it into P[k mod 4] (no separate p update: one read of p less per
 // body), kernel 2 is update_r with the stop rule; in slot 3 it also applies

@@ -233,7 +233,8 @@ int cgx_cg_kernel_exec_times(cgx_cg *cg, double *avg_ms, int64_t *calls);
 /* Tuning knobs (0 = default): iterations per host poll; use hipGraph replay. */
 int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
 /* Iteration structure (before cgx_cg_begin): 0 auto (4 for the 2-D plane
- * march and cache-resident stencil matrices, else 3; the default), 1
+ * march, cache-resident stencil matrices, lean walks of >= 32 M rows and
+ * partitioned lean interiors of <= 4 M rows, else 3; the default), 1
  * three kernels
  * (SpMV+p.Ap, r-update+r.r, x/p-update), 2 fused (single device only): two
  * kernels, the x/p update folded into the next iteration's SpMV (p_j =
@@ -241,11 +242,15 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * twice the gathers; 3 three kernels with the x update deferred: p cycles
  * through four buffers and x += a0 p0 + ... + a3 p3 (in order) runs once
  * per four bodies and at the end of each cgx_cg_run (34 N instead of 40 N
- * bytes per body for the x/p update); 4 fused with deferred x (single
- * device, f64, production SpMV formats): two kernels per body, p_k = r +
+ * bytes per body for the x/p update); 4 fused with deferred x (f64,
+ * production SpMV formats): two kernels per body, p_k = r +
  * beta p_{k-1} computed where the SpMV reads it and stored once into the
  * p ring, update_r with the stop rule, x from the four p buffers in slot 3
- * (72 N + matrix bytes per body against 78 N in mode 3); 5 persistent body
+ * (72 N + matrix bytes per body against 78 N in mode 3); on a partitioned
+ * matrix it needs the device peer transport and the lean interior walk
+ * (three launches: interior walk with the push of the formed p_k, boundary
+ * rows, update_r with both all-reduces; x bit-identical to mode 3; auto at
+ * <= 4 M rows per rank); 5 persistent body
  * (single device, f64; register forms up to 1024 rows per CU, the streamed form
  * up to 8 x 1024 x min(256, CUs) rows): one launch runs a whole chunk of
  * bodies, each with two grid-wide exchanges of the dot partials instead of
