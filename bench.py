@@ -498,8 +498,7 @@ def run(args) -> None:
         why4 = None if t4.item() == 1.0 else "not every rank's interior takes it"
         if why4 is None:
             v4 = validate_peer(L, q, world, rank, dist, nxy=128, mode=4)
-            if validation is not None:
-                validation["mode4"] = v4
+            validation = {**(validation or {}), "mode4": v4}
             if not v4["ok"]:
                 why4 = f"failed its validation ({v4.get('why')})"
         if why4 is not None and me.value == 4:
