@@ -499,6 +499,22 @@ template <typename T, bool NTP = false> struct GatherP {
     return ((const __attribute__((address_space(4))) T *)r)[i] +
            beta * ((const __attribute__((address_space(4))) T *)pp)[i];
   }
+  // pair_b in two halves: the loads (issued a step early by the team walk's
+  // prefetch) and the forming (pair_b's expression, so the same value)
+  struct Raw {
+    typename PairU<T>::V a, q;
+  };
+  __device__ __forceinline__ Raw raw_b(unsigned b) const {
+    using U = typename PairU<T>::V;
+    return Raw{*reinterpret_cast<const U *>(reinterpret_cast<const char *>(r) + b),
+               *reinterpret_cast<const U *>(reinterpret_cast<const char *>(pp) + b)};
+  }
+  __device__ __forceinline__ typename PairU<T>::V form(const Raw &w) const {
+    typename PairU<T>::V o;
+    o.x = w.a.x + beta * w.q.x;
+    o.y = w.a.y + beta * w.q.y;
+    return o;
+  }
 };
 // Mode 4's boundary rows of a partitioned matrix (k_spmv_fd_bnd): own
 // columns form p_k as GatherP, ghosts (from n on) are the neighbours' formed
@@ -1902,13 +1918,24 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
 // 4-wave walk: Ap bit for bit.
 constexpr int kTeamWaves = 16;
 constexpr int kTeamBlock = 64 * kTeamWaves;
+// the team walk's prefetch register (Gather::Raw where it prefetches)
+template <class G, bool PF> struct PfRaw {
+  using type = int;
+};
+template <class G> struct PfRaw<G, true> {
+  using type = typename G::Raw;
+};
 template <typename T> struct TeamLds {
   typename PairU<T>::V pub[2][kTeamWaves][64];  // published centers, double-buffered by step
   SellLds<T> sell;                              // the per-slice form's dictionary, reductions
   T red[kTeamWaves];
 };
 
-template <typename T, class Epi, class Gather>
+// PF: the +-D pair a step ahead of the one the sums use is loaded (raw, in
+// Gather's halves) before the step's barrier and formed the step after, so
+// each wave keeps a load in flight across its barrier, LDS reads, sums and
+// stores instead of waiting a full memory round trip per step
+template <typename T, class Epi, class Gather, bool PF = false>
 __device__ __forceinline__ void spmv_lean_team(const CsrArgs &A, const Gather &x, Epi &epi,
                                                const T *__restrict__ vd,
                                                const unsigned long long *vt, TeamLds<T> &tl) {
@@ -1942,6 +1969,14 @@ __device__ __forceinline__ void spmv_lean_team(const CsrArgs &A, const Gather &x
   unsigned cw = 0;
   PV c_ahead, c_ct;
   int carry_s = -1;
+  typename PfRaw<Gather, PF>::type nraw{};
+  int npos = -1;  // PF: the walk position whose ahead pair nraw holds
+  // the ahead pair's byte offset of the slice at walk position s0
+  [[maybe_unused]] auto ahead_b = [&](int s0) {
+    const int f = (A.rev ? lo + end - 1 - s0 : s0) * (2 * kSellRows);
+    const unsigned r = (unsigned)(f + 2 * lane) * (unsigned)sizeof(T);
+    return A.rev ? r - (f >= D ? oD : 0u) : r + (f + 2 * kSellRows + D <= nxi ? oD : 0u);
+  };
   for (int j = 0; j < trips; ++j) {
     if ((j & 255) == 0) {
       const int k = (j >> 2) + lane;
@@ -1967,10 +2002,28 @@ __device__ __forceinline__ void spmv_lean_team(const CsrArgs &A, const Gather &x
         ct = x.pair_b(rb);
         behind = x.pair_b(A.rev ? opD : omD);
       }
-      ahead = x.pair_b(A.rev ? omD : opD);
+      if constexpr (PF) {
+        ahead = s == npos ? x.form(nraw) : x.pair_b(A.rev ? omD : opD);
+      } else {
+        ahead = x.pair_b(A.rev ? omD : opD);
+      }
       tl.pub[buf][wid][lane] = ct;
     } else if (c == 0xff) {
       tl.pub[buf][wid][lane] = x.pair_b(rb);  // the neighbours' pairs
+    }
+    if constexpr (PF) {  // the next position's ahead pair, in flight across this step
+      int sn;
+      if (P == 0) {
+        sn = s + step;
+      } else {
+        const int zn = zp + 1 == P ? 0 : zp + 1, cn = zp + 1 == P ? cb + step : cb;
+        sn = cn >= K ? end : lo + zn * K + cn + w;
+      }
+      npos = -1;
+      if (sn < end) {
+        nraw = x.raw_b(ahead_b(sn));
+        npos = sn;
+      }
     }
     lds_barrier();
     if (c == 0xff) {
@@ -2574,7 +2627,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
 
 // k_spmv_fd_lean in the team form (CsrDev::vl_team): the published centers
 // are the formed p_k, so an in-team neighbour costs no r / p_{k-1} loads
-template <typename T>
+template <typename T, bool PF>
 __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
     CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
     T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr) {
@@ -2614,7 +2667,7 @@ __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
   }
   const GatherP<T> g{r, pold, beta};
   EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
-  spmv_lean_team<T>(A, g, e, vd, vt, tl);
+  spmv_lean_team<T, EpiFD<T>, GatherP<T>, PF>(A, g, e, vd, vt, tl);
   const T v = team_sum(e.acc, tl.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v;
 }
@@ -4219,9 +4272,11 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
   a.rev = rev;
   if constexpr (std::is_same<T, double>::value) {
     if (vl_whole(A)) {  // the lean walk at its class layout's grid
+      // (the team form with its +-D prefetch: 1,025-1,042 against 1,067-1,079
+      // us per launch at 512^3, profiles/r06b_team_prefetch_ab.log)
       if (A.vl_team)
-        CGX_GGL(k_spmv_fd_lean_t<T>, dim3(A.vl_grid / 4), dim3(kTeamBlock), 0, s, a, r, pold,
-                pc, Ap, st, slot, ws, np_rr);
+        CGX_GGL((k_spmv_fd_lean_t<T, true>), dim3(A.vl_grid / 4), dim3(kTeamBlock), 0, s, a, r,
+                pold, pc, Ap, st, slot, ws, np_rr);
       else
         CGX_GGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc, Ap, st,
                 slot, ws, np_rr);
