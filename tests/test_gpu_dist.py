@@ -110,7 +110,7 @@ def test_partitioned_lean_interior(nproc, transport):
 LEAN = {"CGX_SPMV_VARIANT": "33554432:0"}
 
 
-@pytest.mark.parametrize("nproc", [2, 3])
+@pytest.mark.parametrize("nproc", [2, 3, 4])
 def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     """Mode 4 on the partitioned body (round 5): kernel 1 walks the interior
     forming p_k = r + beta p_{k-1} and pushes the formed p_k of the send rows
@@ -129,6 +129,8 @@ def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     for var, _ in r4["variant_lean_slices"]:
         assert var & 33554432, r4["variant_lean_slices"]
     assert r4["x_sha"] == r3["x_sha"], (r4, r3)
+    if nproc > 2:  # inner ranks: two neighbours, two pushes and two waits per body
+        assert r4["neighbours"][1] == 2, r4["neighbours"]
 
 
 def test_partitioned_mode4_stop_rule_and_resumed_runs():
