@@ -616,7 +616,7 @@ def run(args) -> None:
                             else str(int(variant.value)), mode_eff, team.value)
             roof["traffic_by_kernel"] = t.get("by_kernel")
             roof["traffic_method"] = t.get("method")
-            key = ("k_spmv_fd_lean_t<double, true>" if kname == "k_spmv_fd_lean_t"
+            key = ("k_spmv_fd_lean_t<double, true, true>" if kname == "k_spmv_fd_lean_t"
                    else f"{kname}<double>" if kname.startswith(("k_spmv_lean", "k_spmv_fd_lean"))
                    else f"{kname}<double, {int(variant.value & ~KVL)}>")
             if t.get("by_kernel") and key in t["by_kernel"]:

@@ -2271,7 +2271,7 @@ template <typename T> struct EpiFused {
 // reads it (GatherP, also for the center pair the value-code forms hand to
 // pre2c) and stored once into this body's p buffer; then helper = A p_k and
 // value2 += helper.p_k (CG.hpp:374-379) exactly as EpiDot.
-template <typename T, bool NTP = false> struct EpiFD {
+template <typename T, bool NTP = false, bool NTS = false> struct EpiFD {
   T *__restrict__ Ap;
   T *__restrict__ pc;
   GatherP<T, NTP> g;
@@ -2304,8 +2304,13 @@ template <typename T, bool NTP = false> struct EpiFD {
       a.y = s1;
       q.x = pv;
       q.y = pv1;
-      *reinterpret_cast<PV *>(Ap + i) = a;
-      *reinterpret_cast<PV *>(pc + i) = q;
+      if constexpr (NTS) {  // streams past the Infinity Cache
+        __builtin_nontemporal_store(a, reinterpret_cast<PV *>(Ap + i));
+        __builtin_nontemporal_store(q, reinterpret_cast<PV *>(pc + i));
+      } else {
+        *reinterpret_cast<PV *>(Ap + i) = a;
+        *reinterpret_cast<PV *>(pc + i) = q;
+      }
     } else {
       if (l0) {
         Ap[i] = s0;
@@ -2627,7 +2632,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
 
 // k_spmv_fd_lean in the team form (CsrDev::vl_team): the published centers
 // are the formed p_k, so an in-team neighbour costs no r / p_{k-1} loads
-template <typename T, bool PF>
+template <typename T, bool PF, bool NTS>
 __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
     CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
     T *__restrict__ Ap, CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr) {
@@ -2666,8 +2671,8 @@ __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
     vt = tl.sell.vt;
   }
   const GatherP<T> g{r, pold, beta};
-  EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
-  spmv_lean_team<T, EpiFD<T>, GatherP<T>, PF>(A, g, e, vd, vt, tl);
+  EpiFD<T, false, NTS> e{Ap, pc, g, T(0), T(0), T(0)};
+  spmv_lean_team<T, EpiFD<T, false, NTS>, GatherP<T>, PF>(A, g, e, vd, vt, tl);
   const T v = team_sum(e.acc, tl.red);
   if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v;
 }
@@ -4274,9 +4279,12 @@ hipError_t Launch<T>::spmv_fd(const CsrDev &A, const T *r, const T *pold, T *pc,
     if (vl_whole(A)) {  // the lean walk at its class layout's grid
       // (the team form with its +-D prefetch: 1,025-1,042 against 1,067-1,079
       // us per launch at 512^3, profiles/r06b_team_prefetch_ab.log)
+      // (and its p_k / Ap stores non-temporal: the team form runs walks of >= 32
+      // M rows, whose vectors are past the Infinity Cache; 544-545 against
+      // 532-537 it/s at 512^3, profiles/r06k_team_nt_stores_ab.log)
       if (A.vl_team)
-        CGX_GGL((k_spmv_fd_lean_t<T, true>), dim3(A.vl_grid / 4), dim3(kTeamBlock), 0, s, a, r,
-                pold, pc, Ap, st, slot, ws, np_rr);
+        CGX_GGL((k_spmv_fd_lean_t<T, true, true>), dim3(A.vl_grid / 4), dim3(kTeamBlock), 0, s, a,
+                r, pold, pc, Ap, st, slot, ws, np_rr);
       else
         CGX_GGL(k_spmv_fd_lean<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, r, pold, pc, Ap, st,
                 slot, ws, np_rr);
