@@ -274,7 +274,7 @@ def autotune_record(L, A) -> dict | None:
     """The SpMV autotune's timings of this matrix (cgx_csr_autotune_record):
     every form it timed, how, and its median µs per launch."""
     n = C.c_int(0)
-    if not hasattr(L, "cgx_csr_autotune_record"):  # (an older $CGX_LIB A/B build)
+    if not hasattr(L, "cgx_csr_autotune_record"):  # (an older A/B build, tools/ab_lib.py)
         return None
     L.cgx_csr_autotune_record(A, None, None, None, 0, C.byref(n))
     if n.value == 0:
@@ -440,6 +440,7 @@ def run(args) -> None:
     if args.force_lean:  # the lean walk whatever the autotune chose (tests)
         check(L.cgx_csr_set_variant(A, KVL))
     peer_note = None
+    peer_form = None
     validation = None
     use_peer = world > 1 and args.transport in ("peer", "host-peer")
     if world > 1 and args.transport in ("auto", "host-peer"):
@@ -461,6 +462,9 @@ def run(args) -> None:
         check(L.cgx_dist_peer_enable(A, C.byref(ok)))
         if ok.value:
             transport = "peer (setup: " + transport + ")"
+            coloc, onew = C.c_int(0), C.c_int(0)
+            check(L.cgx_dist_peer_form(A, C.byref(coloc), C.byref(onew)))
+            peer_form = {"colocated": coloc.value, "one_waiter": onew.value}
         elif args.transport != "auto":
             raise SystemExit(f"bench.py: peer transport unavailable: "
                              f"{L.cgx_last_error().decode()}")
@@ -574,7 +578,7 @@ def run(args) -> None:
         # (hipExtLaunchKernel), as rocprofv3 times them; the launch-bracketing
         # pairs where a kernel does not record them
         xcalls = (C.c_int64 * 4)()
-        if hasattr(L, "cgx_cg_kernel_exec_times"):  # (an older $CGX_LIB A/B build lacks it)
+        if hasattr(L, "cgx_cg_kernel_exec_times"):  # (an older A/B build lacks it, tools/ab_lib.py)
             check(L.cgx_cg_kernel_exec_times(cg, avg, xcalls))
         for i in range(4):
             if xcalls[i] == 0:
@@ -670,6 +674,7 @@ def run(args) -> None:
                        "parallelism": f"rows{world}" if world > 1 else "single",
                        "transport": transport,
                        "peer_fallback_reason": peer_note,
+                       "peer_form": peer_form,
                        "rccl_note": rccl_note,
                        "rccl_iteration": rccl_iteration,
                        "transport_validation": validation,

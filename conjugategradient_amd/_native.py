@@ -20,8 +20,10 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# CGX_LIB selects another build of the same library (A/B measurements).
-LIB_PATH = os.environ.get("CGX_LIB") or os.path.join(HERE, "libcgx.so")
+LIB_PATH = os.path.join(HERE, "libcgx.so")
+# (tools/ab_lib.py, the A/B harness, points LIB_PATH at another build and sets
+# this to leave entry points an older build lacks unbound)
+_AB_BUILD = False
 HEADER = os.path.join(os.path.dirname(HERE), "include", "cgx.h")
 
 F64, F32 = 0, 1
@@ -120,6 +122,7 @@ _SIGS = {
     "cgx_dist_allreduce_sum": (_i32, [_vp, C.POINTER(_dbl)]),
     "cgx_dist_peer_enable": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_dist_peer_info": (_i32, [_vp, C.POINTER(_i32)]),
+    "cgx_dist_peer_form": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     # host-only helpers (no device needed)
     "cgx_plan_ghosts": (_i32, [_i64, _i64, _i64, _vp, _i32, _vp, _vp, C.POINTER(_i64),
                                C.POINTER(C.POINTER(_i64)), _vp]),
@@ -150,8 +153,8 @@ def lib() -> C.CDLL:
                            "make -C conjugategradient_amd/csrc")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            if os.environ.get("CGX_LIB") and not hasattr(L, name):
-                continue  # an older A/B build ($CGX_LIB) without this entry point
+            if _AB_BUILD and not hasattr(L, name):
+                continue  # an older A/B build without this entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -227,6 +227,10 @@ int enqueue_spmv_dot(cgx_cg *cg, T *p, int slot, int rev, int *np) {
            else if (split)
              e = Launch<T>::spmv_dot_slices(A->dev, A->d_split, A->split_ni, 0, p, Ap, st, slot,
                                             ws, s, rev);
+           // the one-waiter form: one workgroup waits, the boundary grid does not
+           if (e == hipSuccess && fold && A->peer.one_waiter &&
+               peer_wait_one<T>(A, st, slot, s))
+             e = hipErrorLaunchFailure;
            if (e == hipSuccess && fold)
              return rows ? Launch<T>::spmv_dot_rows(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, p, Ap,
                                                     st, slot, ws, s, &A->peer.dev)
@@ -296,8 +300,10 @@ int dist_dot(cgx_cg *cg, const T *part, int np, T *dst, int slot, int which) {
 // kernels that consume them (update_r: p.Ap, the x/p update: r.r; every
 // workgroup polls the mailboxes, peerdev::world_sum) instead of as two
 // one-workgroup launches (k_peer_allreduce, round 2's form).
+// (the one-waiter form, ranks sharing a GPU: k_peer_allreduce's one
+// workgroup per dot instead, through dist_dot; the same sums)
 static const PeerDev *fused_ar(const cgx_cg *cg) {
-  return (cg->A->dist && cg->A->peer.on) ? &cg->A->peer.dev : nullptr;
+  return (cg->A->dist && cg->A->peer.on && !cg->A->peer.one_waiter) ? &cg->A->peer.dev : nullptr;
 }
 
 template <typename T> int enqueue_iter(cgx_cg *cg, int slot) {
@@ -408,6 +414,8 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
     if ((rc = timed(cg, 1, s, [&] {
            hipError_t e = Launch<T>::spmv_fd_lean_push(A->dev, r, P[(slot + 3) & 3], P[slot], Ap,
                                                        st, slot, ws, s, par, PD, wg0);
+           if (e == hipSuccess && A->peer.one_waiter && peer_wait_one<T>(A, st, slot, s))
+             e = hipErrorLaunchFailure;
            if (e == hipSuccess)
              e = Launch<T>::spmv_fd_rows_bnd(A->dev, A->d_bnd_blk, A->bnd_nblk, gi, r,
                                              P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, s, PD);
@@ -415,8 +423,14 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
          })))
       return rc;
     const int npp = gi + Launch<T>::rows_grid(A->dev, A->bnd_nblk);
+    // the one-waiter form: p.Ap all-reduced by one workgroup into st first
+    // (the partials in sum_parts order, as kernel 3 would); kernel 3 then
+    // reads it from st and only its last workgroup waits (on r.r)
+    const bool one = A->peer.one_waiter;
+    if (one && (rc = peer_allreduce<T>(A, ws->pap_part, npp, &st->pAp[slot], st, slot, s, 1)))
+      return rc;
     return timed(cg, 2, s, [&] {
-      return Launch<T>::update_r_peer_rule(cg->n, r, Ap, st, slot, ws, npp, rpar, x,
+      return Launch<T>::update_r_peer_rule(cg->n, r, Ap, st, slot, ws, one ? 0 : npp, rpar, x,
                                            slot == 3 ? P : nullptr, s, PD);
     });
   }

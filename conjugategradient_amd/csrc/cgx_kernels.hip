@@ -2507,22 +2507,10 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_bnd(
     CgScalars<T> *st, int slot, RedWs<T> *ws, PeerDev P) {
   if (peerdev::skip_body(st, slot, P.state)) return;
   __shared__ int ok_s;
-  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
-  if (threadIdx.x < 64) {
-    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
-    bool ok = true;
-    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
-      ok = ok && peerdev::spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
-                                  P.spin_ticks);
-    ok = __all(ok);
-    if (threadIdx.x == 0) ok_s = ok;
-  }
-  __syncthreads();
-  if (!ok_s) {
+  if (!peerdev::wait_pushes(P, peerdev::body_tag(st, slot, P.state), &ok_s)) {
     if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, as k_peer_wait
   __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherXL<T>{p, reinterpret_cast<const T *>(P.land_local), (int)A.n}, e,
@@ -2727,22 +2715,10 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd_bnd(
     PeerDev P) {
   if (peerdev::skip_body(st, slot, P.state)) return;
   __shared__ int ok_s;
-  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
-  if (threadIdx.x < 64) {
-    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
-    bool ok = true;
-    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
-      ok = ok && peerdev::spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
-                                  P.spin_ticks);
-    ok = __all(ok);
-    if (threadIdx.x == 0) ok_s = ok;
-  }
-  __syncthreads();
-  if (!ok_s) {
+  if (!peerdev::wait_pushes(P, peerdev::body_tag(st, slot, P.state), &ok_s)) {
     if (threadIdx.x == 0) peerdev::raise_fault(st, slot, P.state);
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, as k_peer_wait
   const int prev = (slot + 3) & 3;
   const T beta = st->bodies > 0 ? st->rxr[slot] / st->rxr[prev] : T(0);
   __shared__ LdsOf<T, V> sm;
@@ -2988,7 +2964,9 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     return;
   }
   T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
-  if constexpr (PEER) {
+  // (PEER without partials: the one-waiter form's k_peer_allreduce has put
+  // the world p.Ap into st already)
+  if (PEER && from_parts) {
     __shared__ double wres;
     __shared__ int wok;
     if (P->state->fault) {  // an earlier spin timed out: stop this body too
@@ -3164,7 +3142,11 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer_rule(int64_t n, T *r,
   // short would break the next grid reduction on this workspace)
   __shared__ int lastf;
   if (!last_arrival(ws, &lastf)) return;
-  if (!st->active[slot] || P.state->fault) return;
+  // another workgroup of this launch may have faulted on the p.Ap wait after
+  // this one read the flag: read it again past the cache
+  if (!st->active[slot] ||
+      __hip_atomic_load(&P.state->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    return;
   __shared__ T red[4];
   __shared__ T bc;
   T v[1] = {T(0)};

@@ -88,6 +88,10 @@ struct PeerDev {  // kernel argument (by value)
   int64_t n_local, n_ghost;
   long long spin_ticks;           // wall-clock ticks before a spin gives up
   int rank, world, nsend, nrecv;
+  // one-waiter form (Peer::one_waiter): a one-workgroup k_peer_wait launch
+  // precedes the boundary launch, whose workgroups then skip the flag poll
+  int nopoll;
+  int pad_;
 };
 // mailbox layout inside a rank's ctl allocation: val[2][kPeerMax] doubles,
 // tag[2][kPeerMax] u64 (parity = tag & 1), then flag[kPeerMax][kPushWG] u64
@@ -101,6 +105,16 @@ struct Peer {
   void *state = nullptr;  // PeerState
   std::vector<void *> mapped;  // IPC mappings of other ranks' buffers
   PeerDev dev{};
+  // ranks whose device is this rank's (PCI bus id; 1 on a one-GPU-per-rank
+  // node) and the iteration form taken on every rank (cgx_dist_peer_enable):
+  // in the one-waiter form at most one workgroup per rank waits on another
+  // rank at any time (k_peer_wait with one workgroup before the boundary
+  // launch, k_peer_allreduce before the kernels that consume a dot), so
+  // ranks that share a GPU cannot starve each other of CUs; the fused form
+  // lets whole grids wait, which is safe only when no waiting grid holds the
+  // CUs a peer needs to make progress (DESIGN.md §9 "Ranks sharing a GPU")
+  int colocated = 1;
+  bool one_waiter = false;
 };
 
 // Host-staged transport (cgx_dist_init_host): collectives are callbacks.
@@ -262,6 +276,9 @@ template <typename T> int peer_push(cgx_csr *A, const T *v_ext, CgScalars<T> *st
                                     hipStream_t s);
 template <typename T> int peer_wait(cgx_csr *A, T *v_ext, CgScalars<T> *st, int slot,
                                     hipStream_t s);
+// the one-waiter form's wait: one workgroup polls the push flags (no copy;
+// the boundary launch behind it reads the landing buffer with P.nopoll)
+template <typename T> int peer_wait_one(cgx_csr *A, CgScalars<T> *st, int slot, hipStream_t s);
 // *dst = sum over ranks of (sum of part[0..np)), identical bits on every rank
 // which: 0 setup / init, 1 and 2 the body's p.Ap and r.r (k_peer_allreduce)
 template <typename T> int peer_allreduce(cgx_csr *A, const T *part, int np, T *dst,

@@ -72,28 +72,19 @@ __global__ __launch_bounds__(kBlock) void k_peer_push(const T *__restrict__ v, P
 
 // k_peer_wait: every workgroup's first wave polls the flags of every rank
 // that sends here (all kPushWG of each) for this body's tag, then the
-// workgroup copies its share of the landing buffer into v's ghost area
+// workgroup copies its share of the landing buffer into v's ghost area.
+// v == nullptr (peer_wait_one, one workgroup): the wait alone; the boundary
+// launch behind it reads the landing buffer itself
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_peer_wait(T *__restrict__ v, PeerDev P,
                                                        CgScalars<T> *st, int slot) {
   __shared__ int ok_s;
   if (skip_body(st, slot, P.state)) return;
-  const unsigned long long tag = peerdev::body_tag(st, slot, P.state);
-  if (threadIdx.x < 64) {
-    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
-    bool ok = true;
-    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
-      ok = ok && spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
-                         P.spin_ticks);
-    ok = __all(ok);
-    if (threadIdx.x == 0) ok_s = ok;
-  }
-  __syncthreads();
-  if (!ok_s) {
+  if (!peerdev::wait_pushes(P, peerdev::body_tag(st, slot, P.state), &ok_s)) {
     if (threadIdx.x == 0) raise_fault(st, slot, P.state);
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  if (!v) return;
   const T *land = reinterpret_cast<const T *>(P.land_local);
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < P.n_ghost; k += stride)
@@ -171,10 +162,21 @@ int peer_push(cgx_csr *A, const T *v_ext, CgScalars<T> *st, int slot, hipStream_
 }
 
 template <typename T> int peer_wait(cgx_csr *A, T *v_ext, CgScalars<T> *st, int slot, hipStream_t s) {
-  const PeerDev &P = A->peer.dev;
+  PeerDev P = A->peer.dev;
+  P.nopoll = 0;  // this launch is the one that polls
   if (P.nrecv == 0) return CGX_OK;
-  hipLaunchKernelGGL(k_peer_wait<T>, dim3(wait_grid(P.n_ghost)), dim3(kBlock), 0, s, v_ext, P, st,
-                     slot);
+  // (the one-waiter form: one workgroup polls and copies)
+  hipLaunchKernelGGL(k_peer_wait<T>, dim3(A->peer.one_waiter ? 1 : wait_grid(P.n_ghost)),
+                     dim3(kBlock), 0, s, v_ext, P, st, slot);
+  CGX_HIP(hipGetLastError());
+  return CGX_OK;
+}
+
+template <typename T> int peer_wait_one(cgx_csr *A, CgScalars<T> *st, int slot, hipStream_t s) {
+  PeerDev P = A->peer.dev;
+  P.nopoll = 0;
+  if (P.nrecv == 0) return CGX_OK;
+  hipLaunchKernelGGL(k_peer_wait<T>, dim3(1), dim3(kBlock), 0, s, (T *)nullptr, P, st, slot);
   CGX_HIP(hipGetLastError());
   return CGX_OK;
 }
@@ -192,6 +194,8 @@ template int peer_push<double>(cgx_csr *, const double *, CgScalars<double> *, i
 template int peer_push<float>(cgx_csr *, const float *, CgScalars<float> *, int, hipStream_t);
 template int peer_wait<double>(cgx_csr *, double *, CgScalars<double> *, int, hipStream_t);
 template int peer_wait<float>(cgx_csr *, float *, CgScalars<float> *, int, hipStream_t);
+template int peer_wait_one<double>(cgx_csr *, CgScalars<double> *, int, hipStream_t);
+template int peer_wait_one<float>(cgx_csr *, CgScalars<float> *, int, hipStream_t);
 template int peer_allreduce<double>(cgx_csr *, const double *, int, double *, CgScalars<double> *,
                                     int, hipStream_t, int);
 template int peer_allreduce<float>(cgx_csr *, const float *, int, float *, CgScalars<float> *,
@@ -209,6 +213,8 @@ int peer_destroy(cgx_csr *A) {
     }
   pr.on = false;
   pr.dev = PeerDev{};
+  pr.colocated = 1;
+  pr.one_waiter = false;
   return CGX_OK;
 }
 
@@ -225,6 +231,9 @@ struct PeerCard {
   int64_t recv_cnt[kPeerMax];
   int ok;                      // this rank got this far
   int pad;
+  char bus[32];                // PCI bus id of the rank's device (ranks sharing a GPU)
+  int one_req;                 // $CGX_PEER_ONE_WAITER: -1 unset, 0 fused form, 1 one-waiter
+  int pad2;
 };
 
 int all_ok(cgx_ctx *ctx, int mine, int *all) {
@@ -371,6 +380,10 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
   if (e == hipSuccess) e = hipIpcGetMemHandle(&card.land, pr.land);
   card.ok = e == hipSuccess;
   if (!card.ok) why = std::string("allocation / IPC export: ") + hipGetErrorString(e);
+  if (hipDeviceGetPCIBusId(card.bus, (int)sizeof(card.bus) - 1, ctx->device) != hipSuccess)
+    card.bus[0] = 0;
+  card.one_req = -1;
+  if (const char *env = std::getenv("CGX_PEER_ONE_WAITER")) card.one_req = std::atoi(env) ? 1 : 0;
   std::vector<PeerCard> cards((size_t)world);
   if ((rc = comm_allgather(ctx, &card, sizeof(card), cards.data()))) {
     peer_destroy(A);
@@ -378,6 +391,22 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
   }
   bool ok = true;
   for (const PeerCard &c : cards) ok = ok && c.ok;
+  // ranks sharing this rank's GPU, and the form every rank takes: the
+  // one-waiter form when any two ranks share a device (or any rank asks for
+  // it), the fused form otherwise (or when a rank asks for it and none for
+  // the one-waiter form); every rank sees the same cards, so all agree
+  int colocated = 0, one = -1;
+  bool shared = false;
+  for (int q = 0; q < world; ++q) {
+    const PeerCard &c = cards[q];
+    if (c.bus[0] && std::strncmp(c.bus, card.bus, sizeof(c.bus)) == 0) ++colocated;
+    for (int u = 0; u < q; ++u)
+      shared = shared || (c.bus[0] && std::strncmp(c.bus, cards[u].bus, sizeof(c.bus)) == 0);
+    if (c.one_req == 1) one = 1;
+    if (c.one_req == 0 && one < 0) one = 0;
+  }
+  pr.colocated = std::max(1, colocated);
+  pr.one_waiter = one < 0 ? shared : one == 1;
   PeerDev &P = pr.dev;
   P = PeerDev{};
   P.rank = me;
@@ -467,6 +496,7 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
     return CGX_OK;
   }
   P.spin_ticks = (long long)(secs * clk_khz * 1000.0);
+  P.nopoll = pr.one_waiter ? 1 : 0;
   pr.on = true;
   *enabled = 1;
   return CGX_OK;
@@ -475,5 +505,14 @@ extern "C" int cgx_dist_peer_enable(cgx_csr *A, int *enabled) {
 extern "C" int cgx_dist_peer_info(cgx_csr *A, int *enabled) {
   CGX_REQUIRE(A && enabled, CGX_EINVAL, "NULL argument");
   *enabled = A->peer.on ? 1 : 0;
+  return CGX_OK;
+}
+
+// The peer transport's iteration form (cgx.h): ranks sharing this rank's GPU
+// and whether the one-waiter form runs (see Peer::one_waiter)
+extern "C" int cgx_dist_peer_form(cgx_csr *A, int *colocated, int *one_waiter) {
+  CGX_REQUIRE(A && colocated && one_waiter, CGX_EINVAL, "NULL argument");
+  *colocated = A->peer.on ? A->peer.colocated : 0;
+  *one_waiter = A->peer.on && A->peer.one_waiter ? 1 : 0;
   return CGX_OK;
 }

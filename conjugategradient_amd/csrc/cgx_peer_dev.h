@@ -47,6 +47,29 @@ __device__ __forceinline__ bool spin_ge(const unsigned long long *p, unsigned lo
   return true;
 }
 
+// The workgroup's wait for every sending rank's kPushWG push flags of tag
+// `tag` (the first wave polls, bounded); uniform control flow, false on a
+// timeout. With P.nopoll a one-workgroup k_peer_wait launch has already
+// waited (the one-waiter form): nothing to poll, the kernel boundary orders
+// the landing buffer's reads after it.
+__device__ __forceinline__ bool wait_pushes(const PeerDev &P, unsigned long long tag,
+                                            int *ok_lds) {
+  if (P.nopoll) return true;
+  if (threadIdx.x < 64) {
+    const auto *flags = reinterpret_cast<const unsigned long long *>(P.ctl[P.rank] + kPeerFlagOff);
+    bool ok = true;
+    for (int j = threadIdx.x; j < P.nrecv * kPushWG; j += 64)
+      ok = ok && spin_ge(flags + P.recv_rank[j / kPushWG] * kPushWG + (j % kPushWG), tag,
+                         P.spin_ticks);
+    ok = __all(ok);
+    if (threadIdx.x == 0) *ok_lds = ok;
+  }
+  __syncthreads();
+  if (!*ok_lds) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  return true;
+}
+
 // The world sum of `mine` (this rank's local sum, the same in every
 // workgroup of the calling kernel) for all-reduce tag t: the first workgroup
 // of the kernel to arrive here stores value and tag into every rank's

@@ -350,6 +350,15 @@ int cgx_dist_allreduce_sum(cgx_ctx *ctx, double *value);
  * device-side wait (default 10 s; a timeout stops the solve with an error). */
 int cgx_dist_peer_enable(cgx_csr *csr, int *enabled);
 int cgx_dist_peer_info(cgx_csr *csr, int *enabled);
+/* The peer transport's iteration form: *colocated = ranks whose device is
+ * this rank's (0 when the transport is off), *one_waiter = 1 when at most one
+ * workgroup per rank waits on another rank at any time (a one-workgroup wait
+ * launch before the boundary rows, one-workgroup all-reduces before the
+ * kernels that consume the dots). Taken on every rank when any two ranks
+ * share a GPU, where whole waiting grids could hold the CUs a peer needs;
+ * otherwise the fused form (the waits inside the consuming kernels, fewer
+ * launches). Same values either way. $CGX_PEER_ONE_WAITER=0/1 forces it. */
+int cgx_dist_peer_form(cgx_csr *csr, int *colocated, int *one_waiter);
 
 /* ---- host-only helpers (no device needed; the CPU test-suite drives them) --
  * Halo plan of rows [row_begin, row_begin + n_local) whose global column

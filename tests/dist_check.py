@@ -93,6 +93,9 @@ def main():
         if not peer.value:
             raise SystemExit(f"rank {rank}: peer transport unavailable: "
                              f"{L.cgx_last_error().decode()}")
+    coloc, onew = C.c_int(0), C.c_int(0)
+    if peer.value:
+        check(L.cgx_dist_peer_form(A, C.byref(coloc), C.byref(onew)))
     ghosts, nbrs = C.c_int64(), C.c_int()
     check(L.cgx_csr_halo_info(A, C.byref(ghosts), C.byref(nbrs)))
     ni, nb = C.c_int(), C.c_int()
@@ -130,7 +133,8 @@ def main():
     parts = [None] * world
     dist.all_gather_object(parts, (int(ghosts.value), int(nbrs.value), (ni.value, nb.value),
                                    int(peer.value), int(acalls.value),
-                                   (int(var.value), int(ls.value))))
+                                   (int(var.value), int(ls.value)),
+                                   (int(coloc.value), int(onew.value))))
     # x to rank 0 as tensors, padded to the largest block (gloo gathers
     # equal sizes; blocks differ by at most one row)
     mx = max(counts)
@@ -164,6 +168,7 @@ def main():
                           "split": [p[2] for p in parts], "peer": [p[3] for p in parts],
                           "async_exchanges": [p[4] for p in parts],
                           "variant_lean_slices": [p[5] for p in parts],
+                          "peer_form": [p[6] for p in parts],
                           "x_sha": hashlib.sha256(xg.tobytes()).hexdigest()[:16],
                           "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)

@@ -31,6 +31,9 @@ def _worker(rank, world, port, case, out):
         if case == "poisson3d":
             rp, cl, vl = O.poisson(3, 10, 9, 14)
             tol = 1e-8
+        elif case == "slabs":  # 2 planes per rank at world 8
+            rp, cl, vl = O.poisson(3, 8, 8, 16)
+            tol = 1e-8
         else:
             rp, cl, vl = irregular_spd(4000, seed=21, shift=1.0)
             tol = 1e-8
@@ -41,24 +44,34 @@ def _worker(rank, world, port, case, out):
         x, bodies = D.solve(plan, vl[rp[a]:rp[e]], b[a:e], tol, O, n)
         parts = [None] * world
         dist.all_gather_object(parts, x.tolist())
+        nb = [None] * world
+        dist.all_gather_object(nb, (len(plan["ghosts"]), bodies))
         if rank == 0:
             out.put((np.concatenate([np.array(p) for p in parts]), bodies,
-                     len(plan["ghosts"])))
+                     len(plan["ghosts"]), nb))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,case", [(2, "poisson3d"), (3, "poisson3d"), (2, "irregular")])
+@pytest.mark.parametrize("world,case", [(2, "poisson3d"), (3, "poisson3d"), (2, "irregular"),
+                                        (8, "slabs")])
 def test_distributed_cg_matches_single_process(oracle, world, case):
+    """World 8 is config 4's split (BASELINE.json configs[3]): a 8 x 8 x 16 grid
+    in 2-plane slabs, 6 inner ranks with two neighbours and 2 end ranks."""
     from tests.util import irregular_spd, rel
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     mp.start_processes(_worker, args=(world, _free_port(), case, q), nprocs=world,
                        start_method="spawn", join=True)
-    x, bodies, ghosts = q.get(timeout=60)
+    x, bodies, ghosts, per_rank = q.get(timeout=120)
+    # the ranks agree on the stop (every rank derives the same scalars)
+    assert len({b for _, b in per_rank}) == 1, per_rank
     if case == "poisson3d":
         rp, cl, vl = oracle.poisson(3, 10, 9, 14)
+    elif case == "slabs":
+        rp, cl, vl = oracle.poisson(3, 8, 8, 16)
+        assert [g for g, _ in per_rank] == [64] + [128] * 6 + [64], per_rank
     else:
         rp, cl, vl = irregular_spd(4000, seed=21, shift=1.0)
     b = np.arange(1, len(rp), dtype=np.float64)

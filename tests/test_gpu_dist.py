@@ -63,6 +63,29 @@ def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
     # over hipIpc-mapped memory) passed its self-test on every rank and ran
     # the iteration, graph-captured
     assert r["peer"] == [int(transport.endswith("-peer"))] * nproc
+    if transport.endswith("-peer") and nproc > 1:
+        # every rank shares this one GPU: the one-waiter form runs
+        assert r["peer_form"] == [[nproc, 1]] * nproc, r["peer_form"]
+
+
+@pytest.mark.parametrize("transport,mode", [("host", 0), ("host-peer", 3), ("host-async", 3)])
+def test_eight_way_split(transport, mode):
+    """Config 4's 8-way row split (BASELINE.json configs[3]) as 8 ranks on this
+    one GPU: a 64^3 grid in 8-plane slabs, 6 inner ranks with two neighbours
+    and 2 end ranks with one; 80 bodies at tol 0 against the oracle's
+    iteration (rel 1e-10). (A 1e-8 solve of 64^3 with b_i = i + 1 stops at
+    the rounding floor, ||b|| ~ 8e7, where the body count is noise.)"""
+    r = _run(8, transport, 64, mode, ["--bodies", "80"])
+    assert r["ok"], {k: r[k] for k in ("rel_err", "bodies", "oracle_bodies", "accuracy")}
+    assert r["bodies"] == 80
+    assert r["neighbours"] == [1, 2, 2, 2, 2, 2, 2, 1], r["neighbours"]
+    assert r["ghosts"] == [64 * 64] + [2 * 64 * 64] * 6 + [64 * 64], r["ghosts"]
+    assert all(ni > 0 and nb > 0 for ni, nb in r["split"]), r["split"]
+    assert r["peer"] == [int(transport.endswith("-peer"))] * 8
+    if transport == "host-peer":
+        assert r["peer_form"] == [[8, 1]] * 8, r["peer_form"]
+    if transport == "host-async":
+        assert all(c >= 80 for c in r["async_exchanges"]), r["async_exchanges"]
 
 
 @pytest.mark.parametrize("nproc,grid,mode", [(2, 24, 0), (3, 20, 3)])
@@ -110,7 +133,7 @@ def test_partitioned_lean_interior(nproc, transport):
 LEAN = {"CGX_SPMV_VARIANT": "33554432:0"}
 
 
-@pytest.mark.parametrize("nproc", [2, 3, 4])
+@pytest.mark.parametrize("nproc", [2, 3, 4, 8])
 def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     """Mode 4 on the partitioned body (round 5): kernel 1 walks the interior
     forming p_k = r + beta p_{k-1} and pushes the formed p_k of the send rows
@@ -121,8 +144,9 @@ def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     blocks' grid) and every formed value is mode 3's p update, so x is bit
     for bit mode 3's; 30 bodies at tol 0 against the oracle (rel 1e-10)."""
     args = ["--nxy", "128", "--bodies", "30"]
-    r4 = _run(nproc, "host-peer", 48, 4, args, env=LEAN)
-    r3 = _run(nproc, "host-peer", 48, 3, args, env=LEAN)
+    grid = 64 if nproc == 8 else 48
+    r4 = _run(nproc, "host-peer", grid, 4, args, env=LEAN)
+    r3 = _run(nproc, "host-peer", grid, 3, args, env=LEAN)
     assert r4["ok"] and r3["ok"], (r4, r3)
     assert r4["mode_run"] == 4 and r3["mode_run"] == 3
     assert r4["bodies"] == r3["bodies"] == 30
@@ -131,6 +155,29 @@ def test_partitioned_mode4_bit_identical_to_mode3(nproc):
     assert r4["x_sha"] == r3["x_sha"], (r4, r3)
     if nproc > 2:  # inner ranks: two neighbours, two pushes and two waits per body
         assert r4["neighbours"][1] == 2, r4["neighbours"]
+
+
+@pytest.mark.parametrize("nproc", [2, 8])
+def test_peer_forms_bit_identical(nproc):
+    """The device peer transport's two iteration forms (cgx_dist_peer_form,
+    DESIGN.md §9 "Ranks sharing a GPU"): the fused form waits inside the
+    consuming kernels (every workgroup of the boundary launch polls the push
+    flags, every workgroup of update_r and of the p update polls the dot
+    mailboxes: the 8-GPU node's form), the one-waiter form puts one
+    one-workgroup launch in front of each (k_peer_wait, k_peer_allreduce),
+    which ranks sharing a GPU need. Both sum the same partials in the same
+    order, so x is bit for bit the same, in mode 3 and in mode 4."""
+    args = ["--nxy", "128", "--bodies", "30"]
+    grid = 16 * nproc
+    for mode in (3, 4):
+        rf = _run(nproc, "host-peer", grid, mode, args, env={**LEAN, "CGX_PEER_ONE_WAITER": "0"})
+        ro = _run(nproc, "host-peer", grid, mode, args, env=LEAN)
+        assert rf["ok"] and ro["ok"], (rf, ro)
+        assert rf["peer_form"] == [[nproc, 0]] * nproc, rf["peer_form"]
+        assert ro["peer_form"] == [[nproc, 1]] * nproc, ro["peer_form"]
+        assert rf["mode_run"] == ro["mode_run"] == mode
+        assert rf["bodies"] == ro["bodies"] == 30
+        assert rf["x_sha"] == ro["x_sha"], (mode, rf, ro)
 
 
 def test_partitioned_mode4_stop_rule_and_resumed_runs():
@@ -221,11 +268,8 @@ def test_bench_four_ranks_auto_mode4_validated():
     rows) with the lean interior on every rank: bench.py's auto mode takes the
     partitioned mode 4 only after every rank agreed and it solved a 128 x 128
     slab problem over the peer transport to the setup transport's answer
-    (config.transport_validation.mode4), then times it. (256^3 over 4 ranks
-    sharing this one GPU times out in mode 3 as in mode 4: each rank's
-    boundary launch waits for pushes with its whole grid resident, and four
-    such grids hold the CUs a late rank needs for its push —
-    gpurun_out/r5w, round 5; one rank per GPU has no such contention.)"""
+    (config.transport_validation.mode4), then times it. (256^3 over 4 ranks:
+    test_bench_four_ranks_256_on_one_gpu.)"""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--grid", "128",
            "--steps", "20", "--warmup", "5", "--transport", "host-peer", "--no-cpu",
            "--profile-steps", "0", "--force-lean", "--master-port", str(_port())]
@@ -237,6 +281,28 @@ def test_bench_four_ranks_auto_mode4_validated():
     assert v4["ok"] and v4["peer_mode"] == 4, v4
     assert cfg["iteration"].startswith("3 launches (interior walk forming p_k"), cfg["iteration"]
     assert cfg["peer_fallback_reason"] is None, cfg["peer_fallback_reason"]
+
+
+def test_bench_four_ranks_256_on_one_gpu():
+    """The metric's 256^3 grid over 4 ranks sharing this one GPU (256 x 256 x
+    64 slabs, 4.2 M rows each), the lean interior forced: in round 5 every
+    rank's warm-up timed out in mode 3 and in mode 4, because the boundary
+    launches polled for pushes with their whole grids resident and held the
+    CUs a late rank needed for its push (profiles/r05w_*). The ranks now see
+    that they share a device and run the one-waiter form (one polling
+    workgroup per rank), so the run completes on every rank."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--grid", "256",
+           "--steps", "20", "--warmup", "5", "--transport", "host-peer", "--no-cpu",
+           "--no-general", "--profile-steps", "0", "--force-lean",
+           "--master-port", str(_port())]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = line["config"]
+    assert line["n_gpus"] == 4 and line["steps"] == 20 and line["value"] > 0
+    assert cfg["peer_fallback_reason"] is None, cfg["peer_fallback_reason"]
+    assert cfg["transport"].startswith("peer"), cfg["transport"]
+    assert cfg["peer_form"] == {"colocated": 4, "one_waiter": 1}, cfg.get("peer_form")
 
 
 def test_bench_rccl_iteration_at_world_size_one():
