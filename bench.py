@@ -267,7 +267,25 @@ def cpu_baseline(workload: str, grid, threads: int, budget_s: float, iters: int 
 
 TUNE_KINDS = {0: "k_spmv_dot", 1: "k_spmv_dot (interior slices)", 2: "k_spmv_fd",
               3: "lean walk", 4: "lean walk (interior slices)",
-              5: "k_spmv_fd lean walk, team form"}
+              5: "k_spmv_fd lean walk, team form",
+              6: "the pick so far, re-timed beside the lean walk",
+              7: "boundary rows (CSR-stream launch; added to the interior forms)"}
+
+
+SETUP_PHASES = ("schedule", "sell_plan_pack", "value_codes", "split", "autotune", "rest")
+
+
+def setup_record(L, A, wall_s: float) -> dict:
+    """cgx_csr_create's cost (the matrix's setup, outside the timed region):
+    the wall time of the call and its phases (cgx_csr_setup_times)."""
+    from conjugategradient_amd._native import check
+
+    rec = {"csr_create_s": round(wall_s, 4)}
+    if hasattr(L, "cgx_csr_setup_times"):
+        ms, n = (C.c_double * 6)(), C.c_int(0)
+        check(L.cgx_csr_setup_times(A, ms, 6, C.byref(n)))
+        rec["phases_ms"] = {SETUP_PHASES[k]: round(ms[k], 1) for k in range(min(6, n.value))}
+    return rec
 
 
 def autotune_record(L, A) -> dict | None:
@@ -282,7 +300,8 @@ def autotune_record(L, A) -> dict | None:
     v, k, us = (C.c_int * n.value)(), (C.c_int * n.value)(), (C.c_float * n.value)()
     L.cgx_csr_autotune_record(A, v, k, us, n.value, C.byref(n))
     return {"rule": "median of 5 interleaved rounds of 3 launches per form; a form displaces "
-                    "the more specialised one only when >= 3% faster",
+                    "the more specialised one only when >= 3% faster (a split matrix: its "
+                    "interior forms' times plus the boundary rows' launch)",
             "forms": [{"variant": int(v[i]), "how": TUNE_KINDS.get(k[i], str(k[i])),
                        "us": round(float(us[i]), 2)} for i in range(n.value)]}
 
@@ -429,12 +448,16 @@ def run(args) -> None:
     check(L.cgx_iota(q.handle, F64, b.ptr, n_local, float(row_begin)))
     x.fill(0.0)
     A = C.c_void_p()
+    q.wait()
+    t_setup = time.perf_counter()
     if dist_on:
         check(L.cgx_csr_create_dist(q.handle, n_global, row_begin, n_local, nnz_local,
                                     wl.rows.ptr, wl.cols.ptr, wl.vals.ptr, F64, C.byref(A)))
     else:
         check(L.cgx_csr_create(q.handle, n_local, nnz_local, wl.rows.ptr, wl.cols.ptr,
                                wl.vals.ptr, F64, None, C.byref(A)))
+    q.wait()
+    setup = setup_record(L, A, time.perf_counter() - t_setup)
     if args.lean_team != "auto" and not dist_on:  # A/B of the lean walk's team form
         check(L.cgx_csr_set_lean_team(A, int(args.lean_team)))
     if args.force_lean:  # the lean walk whatever the autotune chose (tests)
@@ -689,6 +712,7 @@ def run(args) -> None:
                                      5: "persistent body (one launch per chunk of bodies, two "
                                         "grid-wide exchanges per body)"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
+                       "setup": setup,
                        "spmv_variant": int(variant.value),
                        "spmv_autotune": autotune,
                        "value_code_templates": (

@@ -76,6 +76,7 @@ _SIGS = {
                                  C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "cgx_csr_autotune_record": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32),
                                        C.POINTER(C.c_float), _i32, C.POINTER(_i32)]),
+    "cgx_csr_setup_times": (_i32, [_vp, C.POINTER(_dbl), _i32, C.POINTER(_i32)]),
     "cgx_csr_set_lean_team": (_i32, [_vp, _i32]),
     "cgx_csr_lean_team": (_i32, [_vp, C.POINTER(_i32)]),
     "cgx_csr_march_info": (_i32, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
@@ -135,6 +136,10 @@ _SIGS = {
     "cgx_sellp_plan": (_i32, [_vp, _vp, _i64, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
                               C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
                               C.POINTER(_i32)]),
+    "cgx_sellp_plan_device": (_i32, [_vp, _vp, _vp, _i64, _i64, C.POINTER(_i64),
+                                     C.POINTER(C.POINTER(_i64)), C.POINTER(_i64),
+                                     C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
+                                     C.POINTER(_i32)]),
     "cgx_sell_plan": (_i32, [_vp, _vp, _i64, _i32, C.POINTER(_i64), C.POINTER(C.POINTER(_i64)),
                              C.POINTER(_i64), C.POINTER(C.POINTER(_i32)), C.POINTER(_i64),
                              C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(_i64)]),

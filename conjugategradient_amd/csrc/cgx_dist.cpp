@@ -497,6 +497,7 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   hipStream_t s = ctx->stream;
   const int world = ctx->world, me = ctx->rank;
   int rc;
+  const auto t_start = std::chrono::steady_clock::now();
   // 1. every rank's row range
   std::vector<int64_t> part(2 * (size_t)world, 0);
   const int64_t mine[2] = {row_begin, n_local};
@@ -628,10 +629,14 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
   // the boundary slices are placeholders in the SELL copy (their rows may be
   // unsorted locally: ghosts from lower ranks are numbered after the own
   // rows); the boundary launch runs their rows as CSR-stream blocks
+  setup_begin(A);
+  A->setup_last = t_start;
+  setup_mark(A, 0);
   if ((rc = build_sell(A, hrp.data(), hcol.data(), 0, h.n_ghost > 0 ? &bslice : nullptr))) {
     cgx_csr_destroy(A);
     return rc;
   }
+  setup_mark(A, 2);
   // interior / boundary slices of the SELL copy: the halo exchange overlaps
   // the interior ones (enqueue_iter); a slab of a stencil has one boundary
   // plane per neighbour. Built before the autotune, which times the SELL
@@ -700,10 +705,12 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
       }
     }
   }
+  setup_mark(A, 3);
   if ((rc = autotune_spmv(A))) {
     cgx_csr_destroy(A);
     return rc;
   }
+  setup_mark(A, 4);
   if (!A->dev.sl) A->split_bd_h.clear();  // a CSR-stream form won: no split
   // a lean loop SpMV walks the interior only (the boundary slices are the
   // boundary launch's)
@@ -711,6 +718,8 @@ extern "C" int cgx_csr_create_dist(cgx_ctx *ctx, int64_t n_global, int64_t row_b
     cgx_csr_destroy(A);
     return rc;
   }
+  setup_mark(A, 5);
+  A->setup_open = false;
   *out = A;
   return CGX_OK;
 }

@@ -436,4 +436,10 @@ std::vector<int> build_row_blocks(const int *rowptr, int64_t n, int *max_row_nnz
 
 __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, int64_t row);
 
+// the SELL-P plan's per-slice patterns on the device (k_sellp_plan): w[q]
+// width (kSellPatMax + 1: too many offsets, -1: an unsorted row outside
+// skip), pat[q * kSellPatMax ...] the ascending offsets
+hipError_t sellp_plan_dev(int64_t n, int64_t nsl, const int *rowptr, const int *col,
+                          const char *skip, int *pat, int *w, hipStream_t s);
+
 }  // namespace cgx

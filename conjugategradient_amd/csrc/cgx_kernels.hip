@@ -3390,6 +3390,67 @@ __global__ __launch_bounds__(kBlock) void k_sellp_pack(int64_t n, int64_t nsl,
   }
 }
 
+// SELL-P plan on the device (cgx_abi.cpp sellp_plan_device; the host
+// restatement is sellp_plan_host, which the CPU tests and cgx_sellp_plan
+// keep): one wave per 128-row slice (2 rows per lane, as the SELL-P layout)
+// forms the ascending union of its rows' (col - row) offsets by repeated
+// wave minima above the last offset taken (at most kSellPatMax + 1 rounds),
+// and checks that every row has strictly ascending columns (slices marked in
+// skip are exempt). w[q]: the pattern's width (0: no entries), kSellPatMax +
+// 1 when it has more offsets, -1 for an unsorted row; pat[q * kSellPatMax +
+// j]: the offsets. No column array crosses to the host (256^3: 468 MB).
+__global__ __launch_bounds__(kBlock) void k_sellp_plan(int64_t n, int64_t nsl,
+                                                       const int *__restrict__ rowptr,
+                                                       const int *__restrict__ col,
+                                                       const char *__restrict__ skip,
+                                                       int *__restrict__ pat,
+                                                       int *__restrict__ w) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (q >= nsl) return;  // wave-uniform
+  const int64_t i0 = q * 2 * kSellRows + 2 * lane;
+  int a[2], e[2];
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    a[r] = e[r] = 0;
+    if (i0 + r < n) {
+      a[r] = rowptr[i0 + r];
+      e[r] = rowptr[i0 + r + 1];
+    }
+    for (int k = a[r] + 1; k < e[r]; ++k) bad = bad || col[k] <= col[k - 1];
+  }
+  if (__any(bad) && !(skip && skip[q])) {
+    if (lane == 0) w[q] = -1;
+    return;
+  }
+  long long last = LLONG_MIN;
+  int cnt = 0;
+  for (;;) {
+    long long m = LLONG_MAX;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      for (int k = a[r]; k < e[r]; ++k) {
+        const long long off = (long long)col[k] - (i0 + r);
+        if (off > last && off < m) m = off;
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long t = __shfl_xor(m, o, 64);
+      m = t < m ? t : m;
+    }
+    if (m == LLONG_MAX) break;
+    if (cnt == kSellPatMax) {
+      cnt = kSellPatMax + 1;
+      break;
+    }
+    if (lane == 0) pat[q * kSellPatMax + cnt] = (int)m;
+    ++cnt;
+    last = m;
+  }
+  if (lane == 0) w[q] = cnt;
+}
+
 // SELL-P value codes: the slot layout of k_sellp_pack, each stored value
 // replaced by its index in the sorted dictionary `dict` of nd bit patterns
 // (binary search on the bits: -0.0 / 0.0 and NaN payloads stay distinct);
@@ -3579,6 +3640,14 @@ inline CsrArgs args(const CsrDev &A) {
 }
 
 }  // namespace
+
+hipError_t sellp_plan_dev(int64_t n, int64_t nsl, const int *rowptr, const int *col,
+                          const char *skip, int *pat, int *w, hipStream_t s) {
+  const int64_t per = kBlock / 64;
+  CGX_GGL(k_sellp_plan, dim3((unsigned)((nsl + per - 1) / per)), dim3(kBlock), 0, s, n, nsl,
+          rowptr, col, skip, pat, w);
+  return hipGetLastError();
+}
 
 // number of stored entries in rows [0, row) of the Poisson matrix
 __host__ __device__ int64_t poisson_row_offset(int dim, int nx, int ny, int nz, int64_t row) {

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdint>
 #include <map>
@@ -206,6 +207,12 @@ struct cgx_csr {
   int64_t sell_padded = 0;
   int64_t sell_idx_words = 0;  // dictionary SELL index words
   int64_t vc_chunks = 0;       // value-code chunk-lanes (16 B each, 8 B in 4-bit form)
+  // setup cost by phase (cgx_csr_setup_times): 0 schedule / halo plan,
+  // 1 SELL plan + pack, 2 value codes + templates, 3 interior / boundary
+  // split, 4 SpMV autotune (lean layouts included), 5 the rest; wall ms
+  double setup_ms[6] = {0, 0, 0, 0, 0, 0};
+  bool setup_open = false;
+  std::chrono::steady_clock::time_point setup_last{};
 };
 
 struct cgx_cg {
@@ -254,6 +261,18 @@ struct cgx_cg {
 };
 
 namespace cgx {
+// setup phase timing (cgx_csr::setup_ms): the wall time since the last mark
+// is charged to `phase` while cgx_csr_create(_dist) runs
+inline void setup_begin(cgx_csr *A) {
+  A->setup_open = true;
+  A->setup_last = std::chrono::steady_clock::now();
+}
+inline void setup_mark(cgx_csr *A, int phase) {
+  if (!A->setup_open) return;
+  const auto now = std::chrono::steady_clock::now();
+  A->setup_ms[phase] += std::chrono::duration<double, std::milli>(now - A->setup_last).count();
+  A->setup_last = now;
+}
 // reference counts (cgx_abi.cpp): retain on a handle made from the object,
 // release when that handle (or the owner) lets go; the last release frees
 void ctx_retain(cgx_ctx *ctx);

@@ -148,8 +148,18 @@ int cgx_csr_lean_info(cgx_csr *csr, int *classes, int64_t *slices, int *grid, in
 #define CGX_TUNE_LEAN 3         /* the lean walk over the whole matrix */
 #define CGX_TUNE_LEAN_INTERIOR 4 /* the lean walk over a split matrix's interior */
 #define CGX_TUNE_LEAN_TEAM 5     /* mode 4's fused walk, team form (cgx_csr_set_lean_team) */
+#define CGX_TUNE_INCUMBENT 6     /* the pick before the lean walk's rounds, re-timed in them */
+#define CGX_TUNE_BOUNDARY 7      /* a split matrix's boundary rows (CSR-stream launch), added
+                                    to its interior forms' times before the pick */
 int cgx_csr_autotune_record(cgx_csr *csr, int *variants, int *kinds, float *us, int cap,
                             int *count);
+/* The setup cost of cgx_csr_create / cgx_csr_create_dist by phase, wall
+ * milliseconds (*count = 6; up to `cap` written): [0] row-block schedule (and
+ * the halo plan of a partitioned matrix), [1] SELL plan and pack, [2] value
+ * codes and templates, [3] interior / boundary split, [4] SpMV autotune
+ * (lean layouts included), [5] the rest. Replaces nothing in the reference
+ * (Matrix::init only uploads, LinearAlgebraTypes.hpp:101-121). */
+int cgx_csr_setup_times(cgx_csr *csr, double *ms, int cap, int *count);
 /* Mode 4's fused lean walk (k_spmv_fd_lean) in its team form: 1,024-thread
  * workgroups whose 16 waves share their slices' formed p_k neighbour pairs
  * through LDS instead of gathering r and p_{k-1} for them.
@@ -405,6 +415,14 @@ int cgx_mm_write_lower(const char *path, int64_t n, const int *rowptr, const int
 int cgx_sellp_plan(const int *h_rowptr, const int *h_col, int64_t n, int64_t *nsl,
                    int64_t **slices, int64_t *npat, int **pat, int64_t *value_slots,
                    int *max_width);
+/* The same plan formed on the device (cgx_csr_create's own path since round
+ * 6): k_sellp_plan builds each slice's pattern with one wave, so the column
+ * array never crosses to the host; the pattern pool, offsets and padding
+ * bound follow on the host as above. Outputs as cgx_sellp_plan (free with
+ * cgx_free_host). Needs a device. */
+int cgx_sellp_plan_device(cgx_ctx *ctx, const int *d_rowptr, const int *d_col, int64_t n,
+                          int64_t nnz, int64_t *nsl, int64_t **slices, int64_t *npat, int **pat,
+                          int64_t *value_slots, int *max_width);
 int cgx_sell_plan(const int *h_rowptr, const int *h_col, int64_t n, int rows_per_lane,
                   int64_t *nsl,
                   int64_t **slices, int64_t *ndict, int **dict, int64_t *nidx,

@@ -48,7 +48,9 @@ def main():
                          "iteration (cgx_dist_peer_enable; must pass its self-test); "
                          "'host-async': the host exchange on the comm stream, overlapped "
                          "with the interior slices (cgx_dist_host_async)")
-    ap.add_argument("--mode", type=int, default=0, help="cgx_cg_set_mode (0 auto, 1, 3, 4)")
+    ap.add_argument("--mode", default="0",
+                    help="cgx_cg_set_mode (0 auto, 1, 3, 4); a comma list gives rank r the "
+                         "r-th entry (mixed modes across ranks)")
     ap.add_argument("--runs", type=int, default=1,
                     help="split the solve into this many cgx_cg_run calls after one "
                          "cgx_cg_begin (each run ends with its end-of-run flush)")
@@ -113,7 +115,8 @@ def main():
     x.fill(0.0)
     cg = C.c_void_p()
     check(L.cgx_cg_create(q.handle, A, C.byref(cg)))
-    check(L.cgx_cg_set_mode(cg, a.mode))
+    modes = [int(m) for m in str(a.mode).split(",")]
+    check(L.cgx_cg_set_mode(cg, modes[rank % len(modes)]))
     bodies, rxr = C.c_int64(), C.c_double()
     tol = 0.0 if a.bodies >= 0 else a.tol
     if a.runs > 1:
@@ -126,6 +129,8 @@ def main():
         check(L.cgx_cg_solve(cg, b.ptr, x.ptr, tol, a.bodies, C.byref(bodies), C.byref(rxr)))
     mode_run = C.c_int()
     check(L.cgx_cg_get_mode(cg, C.byref(mode_run)))
+    modes_run = [None] * world
+    dist.all_gather_object(modes_run, int(mode_run.value))
     acalls = C.c_int64()
     check(L.cgx_csr_halo_async_calls(A, C.byref(acalls)))
     acc = C.c_double()
@@ -160,7 +165,7 @@ def main():
         ok = bool(relerr <= 1e-10 and abs(bodies.value - oracle_bodies) <= 2
                   and np.isfinite(xg).all())
         print(json.dumps({"world": world, "transport": a.transport, "mode": a.mode,
-                          "mode_run": mode_run.value, "runs": a.runs,
+                          "mode_run": mode_run.value, "modes_run": modes_run, "runs": a.runs,
                           "grid": [gxy, gxy, g], "bodies": bodies.value,
                           "oracle_bodies": oracle_bodies, "rel_err": relerr,
                           "accuracy": acc.value, "ghosts": [p[0] for p in parts],

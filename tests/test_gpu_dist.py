@@ -180,6 +180,24 @@ def test_peer_forms_bit_identical(nproc):
         assert rf["x_sha"] == ro["x_sha"], (mode, rf, ro)
 
 
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_partitioned_mixed_modes_agree(form):
+    """Auto mode decides per rank (each rank's own autotune), so ranks can run
+    mode 3 and mode 4 side by side: both modes push, wait and
+    all-reduce with the same tags per body (push / wait at the body's base,
+    p.Ap at base + 1, r.r at base + 2, the stop rule on the starting r.r).
+    Rank 0 in mode 3, rank 1 in mode 4, to tolerance: the same bodies and x
+    bit for bit as both ranks in mode 3, in both peer forms."""
+    args = ["--nxy", "128"]
+    env = {**LEAN, "CGX_PEER_ONE_WAITER": form}
+    rm = _run(2, "host-peer", 48, "3,4", args, env=env)
+    r3 = _run(2, "host-peer", 48, 3, args, env=env)
+    assert rm["ok"] and r3["ok"], (rm, r3)
+    assert rm["modes_run"] == [3, 4] and r3["modes_run"] == [3, 3]
+    assert rm["bodies"] == r3["bodies"]
+    assert rm["x_sha"] == r3["x_sha"], (rm, r3)
+
+
 def test_partitioned_mode4_stop_rule_and_resumed_runs():
     """The stop rule and the run boundaries of partitioned mode 4: solved to
     tolerance, and the same solve split into cgx_cg_run calls of 40 bodies
