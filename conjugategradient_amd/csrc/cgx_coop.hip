@@ -578,28 +578,35 @@ hipError_t cg_coop(int64_t n, int R, bool streamed, const int *rowptr, const int
   if (streamed ? (R < 1 || R > kCoopStreamMaxR) : R != 1) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cw, 0, sizeof(CoopWs), s);
   if (e != hipSuccess) return e;
-#define CGX_COOP_FIT(K) \
-  if (!coop_resident((const void *)K, NT, G)) return hipErrorCooperativeLaunchTooLarge
+  const void *fn = nullptr;
   if (!streamed) {
-    CGX_COOP_FIT((k_cg_coop_wt<1, NT>));
-    k_cg_coop_wt<1, NT><<<G, NT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw,
-                                         ticks, trace, nap, stall);
-    return hipGetLastError();
+    fn = (const void *)k_cg_coop_wt<1, NT>;
+  } else {
+    switch (R) {
+      case 1: fn = (const void *)k_cg_coop_st<1>; break;
+      case 2: fn = (const void *)k_cg_coop_st<2>; break;
+      case 3: fn = (const void *)k_cg_coop_st<3>; break;
+      case 4: fn = (const void *)k_cg_coop_st<4>; break;
+      case 5: fn = (const void *)k_cg_coop_st<5>; break;
+      case 6: fn = (const void *)k_cg_coop_st<6>; break;
+      case 7: fn = (const void *)k_cg_coop_st<7>; break;
+      case 8: fn = (const void *)k_cg_coop_st<8>; break;
+      default: return hipErrorInvalidValue;
+    }
   }
-#define CGX_COOP_ST(RR)                                                                     \
-  case RR:                                                                                  \
-    CGX_COOP_FIT(k_cg_coop_st<RR>);                                                         \
-    k_cg_coop_st<RR><<<G, NT, 0, s>>>(n, rowptr, col, val, x, r, p0, p1, st, slot0, m, cw,   \
-                                      ticks, trace, nap, stall);                            \
-    break;
-  switch (R) {
-    CGX_COOP_ST(1) CGX_COOP_ST(2) CGX_COOP_ST(3) CGX_COOP_ST(4)
-    CGX_COOP_ST(5) CGX_COOP_ST(6) CGX_COOP_ST(7) CGX_COOP_ST(8)
-    default: return hipErrorInvalidValue;
-  }
-#undef CGX_COOP_ST
-#undef CGX_COOP_FIT
-  return hipGetLastError();
+  // (the occupancy check first: a refusal then names the cause before the
+  // runtime's own)
+  if (!coop_resident(fn, NT, G)) return hipErrorCooperativeLaunchTooLarge;
+  // A cooperative launch (verdict r5): the runtime guarantees that all G
+  // workgroups are resident together, which the two grid-wide exchanges per
+  // body need; a plain launch only had the occupancy estimate above, and any
+  // other work on the device could hold a CU a late workgroup needed. Mode 5
+  // runs outside the iteration graphs (graph_ok), so capture is not needed.
+  void *args[] = {(void *)&n,  (void *)&rowptr, (void *)&col,   (void *)&val,
+                  (void *)&x,  (void *)&r,      (void *)&p0,    (void *)&p1,
+                  (void *)&st, (void *)&slot0,  (void *)&m,     (void *)&cw,
+                  (void *)&ticks, (void *)&trace, (void *)&nap, (void *)&stall};
+  return hipLaunchCooperativeKernel(fn, dim3(G), dim3(NT), args, 0, s);
 }
 
 }  // namespace cgx
