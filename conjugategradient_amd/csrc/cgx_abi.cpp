@@ -887,6 +887,36 @@ static void free_col16(cgx_csr *A) {
   A->d_col16 = nullptr;
   A->dev.col16 = nullptr;
 }
+// The interleaved val / col copy of the CSR-stream forms (kIL; round 6,
+// verdict r5 item 3): the values and columns of each chunk of kIlCh pairs
+// side by side in one allocation (cgx_internal.h), so the loop reads one
+// stream instead of two arrays whose relative placement moved the kernel by
+// +-15% (DESIGN.md §8 "Round 5"). Built on demand; the matrix's own arrays
+// stay the caller's.
+static void free_il(cgx_csr *A) {
+  if (A->d_il) (void)hipFree(A->d_il);
+  A->d_il = nullptr;
+  A->dev.il = nullptr;
+}
+static bool build_il(cgx_csr *A) {
+  if (A->dev.il) return true;
+  if (A->dev.nnz < 2) return false;
+  hipStream_t s = A->ctx->stream;
+  const int es = (int)dtype_size(A->dtype);
+  void *d = nullptr;
+  hipError_t e = hipMalloc(&d, (size_t)il_bytes(A->dev.nnz, es));
+  if (e == hipSuccess) e = il_build(A->dev, es, (char *)d, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    if (d) (void)hipFree(d);
+    (void)hipGetLastError();
+    return false;
+  }
+  A->d_il = d;
+  A->dev.il = (const char *)d;
+  return true;
+}
+
 static bool build_col16(cgx_csr *A) {
   if (A->dev.col16) return true;
   if (A->dev.nnz < 2 || A->dev.nrb < 1 || !A->dev.rb || !A->dev.rbk) return false;
@@ -1117,6 +1147,7 @@ static void csr_free(cgx_csr *A) {
     if (A->d_ext) (void)hipFree(A->d_ext);
     free_sell(A);
     free_col16(A);
+    free_il(A);
     free_block_order(A);
     peer_destroy(A);
     dist_destroy_halo(A);
@@ -2258,6 +2289,8 @@ extern "C" int cgx_csr_stream_bytes(cgx_csr *A, int64_t *bytes) {
     *bytes = es * A->sell_padded + nsl * 2 * kSellRows * ((v & 16384) ? 4 : 1) + desc;
   else if (v & 2048)
     *bytes = es * A->sell_padded + 8 * A->sell_idx_words + desc;
+  else if (v & kIL)  // the interleaved copy's pairs (a block's first pair may be shared)
+    *bytes = (2 * es + 8) * ((A->dev.nnz + 1) / 2) + 4 * (A->dev.n + 1);
   else
     *bytes = (es + ((v & kC16) ? 2 : 4)) * A->dev.nnz + 4 * (A->dev.n + 1);
   return CGX_OK;
@@ -2395,6 +2428,11 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
               "variant %d needs 4-bit value codes (at most 15 distinct values)", variant);
   CGX_REQUIRE(!(variant & kVT) || A->dev.sl_t, CGX_EUNSUPPORTED,
               "variant %d needs value-code templates, which this matrix does not have", variant);
+  if (variant & kIL) {
+    DeviceGuard g(A->ctx->device);
+    CGX_REQUIRE(build_il(A), CGX_EUNSUPPORTED,
+                "variant %d: the interleaved val / col copy could not be built", variant);
+  }
   if ((variant & kC16) && !(variant & 8192)) {
     DeviceGuard g(A->ctx->device);
     CGX_REQUIRE(build_col16(A), CGX_EUNSUPPORTED,
@@ -2509,6 +2547,10 @@ int autotune_spmv(cgx_csr *A) {
   std::vector<int> cands = big ? std::vector<int>{15} : std::vector<int>{13, 15, 5, 265};
   // and the paired loop on 16-bit column deltas (10 B per entry) where they fit
   if (!big && build_col16(A)) cands.push_back(133);
+  // (the pipelined paired loop on the interleaved val / col copy, kIL, is
+  // not a candidate: 376 against 373 us at 256^3, 25.3 against 24.9 on the
+  // G3 stand-in, 306 against 297 at 4096^2, its stream-only ablation 336
+  // against 324 — profiles/r06f_tune_il_*.log; reachable by request)
   if (A->dev.sl) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
@@ -2737,6 +2779,7 @@ int autotune_spmv(cgx_csr *A) {
     return CGX_EHIP;
   }
   if (lean_G > 0) {
+    free_il(A);
     // (a split matrix keeps its boundary marks and vl_split)
     if (int rc = build_lean_layout(A, vtab, lean_G)) return rc;
     A->dev.variant = kVlBase;
@@ -2748,6 +2791,7 @@ int autotune_spmv(cgx_csr *A) {
   A->dev.variant = best_v;
   if (!(best_v & (2048 | 8192))) free_sell(A);
   if (!(best_v & kC16) || (best_v & 8192)) free_col16(A);
+  if (!(best_v & kIL)) free_il(A);
   return CGX_OK;
 }
 
@@ -3205,13 +3249,16 @@ extern "C" int cgx_cg_begin(cgx_cg *cg, const void *b, void *x, double tol,
   });
   if (rc) return rc;
   if (A->dist && A->peer.on) {
-    // the init kernel left the local r.r in rxr[0]; all-reduce it in place
+    // the init kernel left the local r.r's double-length pair in rr_part[0..1]
+    // (and its value in rxr[0]); all-reduce the pair into rxr[0]
     if (cg->dtype == CGX_F32) {
       auto *st = (CgScalars<float> *)cg->st;
-      rc = peer_allreduce<float>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s, 0);
+      rc = peer_allreduce<float>(A, ((RedWs<float> *)cg->ws)->rr_part, 1, &st->rxr[0], nullptr,
+                                 0, s, 0);
     } else {
       auto *st = (CgScalars<double> *)cg->st;
-      rc = peer_allreduce<double>(A, &st->rxr[0], 1, &st->rxr[0], nullptr, 0, s, 0);
+      rc = peer_allreduce<double>(A, ((RedWs<double> *)cg->ws)->rr_part, 1, &st->rxr[0],
+                                  nullptr, 0, s, 0);
     }
     if (rc) return rc;
   } else if (A->dist) {

@@ -66,8 +66,9 @@ template <typename T> struct RedWs {
   T partials[kMaxRed * kMaxGrid];
   // per-workgroup partials of the iteration's two dots, summed by the NEXT
   // kernel (every workgroup, fixed order): no tail chain in the producer
-  T pap_part[2 * kMaxGrid];  // room for the interior + boundary launches of a split SpMV
-  T rr_part[2 * kMaxGrid];
+  // (each partial a double-length pair hi, lo: cgx_kernels.hip Dd)
+  T pap_part[4 * kMaxGrid];  // room for the interior + boundary launches of a split SpMV
+  T rr_part[4 * kMaxGrid];
 };
 
 // SELL copy of a matrix (built by cgx_csr_create when the matrix qualifies,
@@ -106,6 +107,16 @@ constexpr int kVT = 8388608;
 // CSR-stream with 16-bit column deltas (bit 128 on the paired loop: 133 =
 // 5 | 128): 10 bytes per entry instead of 12
 constexpr int kC16 = 128;
+// CSR-stream on the interleaved copy of val / col (variant bit kIL on the
+// pipelined paired loop: 15 | kIL, 13 | kIL; round 6): the value pairs and
+// column pairs of each chunk of kIlCh consecutive pairs (2 kIlCh entries)
+// side by side in one array, kIlCh x 16 B of values then kIlCh x 8 B of
+// columns; the same 12 B per entry as the two CSR arrays, one stream instead
+// of two independently placed ones
+constexpr int kIL = 67108864;
+constexpr int kIlLog = 8;
+constexpr int kIlCh = 1 << kIlLog;          // pairs per chunk
+constexpr int64_t kIlChBytes = kIlCh * 24;  // 6 KiB (f64)
 constexpr int kVtMax = 8;
 constexpr int kVtWidthMask = 0xffff;
 // Lean stencil walk (variant bit kVL; DESIGN.md §4 "lean stencil walk"): a
@@ -186,6 +197,9 @@ struct CsrDev {
   // block b stores col[k] - rb[b] (every such delta fits int16; null when
   // one does not or the copy was not built)
   const short *col16 = nullptr;
+  // the interleaved val / col copy of the CSR-stream forms (kIL; null when
+  // not built): chunk c at c * kIlChBytes (f64; half the value bytes for f32)
+  const char *il = nullptr;
   // lean stencil walk (kVL, cgx_abi.cpp build_lean): the class bytes in the
   // wave-major layout of a vl_grid-workgroup launch (vl_nst bytes per wave),
   // the class table, the stencil's D and a; `lean`: the loop's SpMV runs it
@@ -419,6 +433,13 @@ hipError_t vc_match(const CsrDev &A, const unsigned long long *tmpl, int nt, Sel
 // the 16-bit column deltas of A's row blocks into col16 (nnz + 2 entries);
 // *bad counts the entries whose delta does not fit
 hipError_t col16_build(const CsrDev &A, short *col16, unsigned *bad, hipStream_t s);
+// the interleaved val / col copy (kIL) of A's CSR arrays into il
+// ((nnz + 1) / 2 pairs, padded to whole chunks); element size es (4 / 8)
+hipError_t il_build(const CsrDev &A, int es, char *il, hipStream_t s);
+inline int64_t il_bytes(int64_t nnz, int es) {
+  const int64_t pairs = (nnz + 1) / 2, chunks = (pairs + kIlCh - 1) / kIlCh;
+  return chunks * kIlCh * (2 * es + 8);
+}
 
 // the SpMV variant a launch on A uses (dtype: CGX_F64 / CGX_F32)
 int launch_variant(const CsrDev &A, int dtype);

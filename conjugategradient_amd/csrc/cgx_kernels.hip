@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "cgx_dd.h"
 #include "cgx_internal.h"
 #include "cgx_objects.h"
 #include "cgx_peer_dev.h"
@@ -119,19 +120,63 @@ __device__ __forceinline__ void block_sum(T (&v)[K], T *lds) {
   __syncthreads();
 }
 
+// Fixed-order workgroup sum of one pair per thread; valid in thread 0.
+// lds: 2 T per wave (8 for a 256-thread workgroup).
+template <typename T> __device__ __forceinline__ Dd<T> block_sum_dd(Dd<T> v, T *lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int W = kBlock / 64;
+  v = wave_sum_dd(v);
+  if (lane == 0) {
+    lds[2 * w] = v.hi;
+    lds[2 * w + 1] = v.lo;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    v = Dd<T>(lds[0], lds[1]);
+#pragma unroll
+    for (int k = 1; k < W; ++k) v += Dd<T>(lds[2 * k], lds[2 * k + 1]);
+  }
+  __syncthreads();
+  return v;
+}
+
+// A workgroup's partial of a dot: slot i of part holds the pair (hi at 2 i,
+// lo at 2 i + 1). Uniform control flow; thread 0 stores.
+template <typename T>
+__device__ __forceinline__ void store_part(T *part, int i, Dd<T> v, T *lds) {
+  v = block_sum_dd(v, lds);
+  if (threadIdx.x == 0) {
+    part[2 * i] = v.hi;
+    part[2 * i + 1] = v.lo;
+  }
+}
+template <typename T> __device__ __forceinline__ Dd<T> load_part(const T *part, int i) {
+  using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+  const V v = *reinterpret_cast<const V *>(part + 2 * i);
+  return Dd<T>(v.x, v.y);
+}
+
 // Sum of the previous kernel's per-workgroup partials, in the same fixed
-// order in every workgroup (thread t: t, t + 256, ...; then block_sum), so
-// all workgroups get the identical value. Stream order makes the producer's
-// plain stores visible; no atomics, no write-through. Uniform control flow.
+// order in every workgroup (thread t: t, t + 256, ...; then block_sum_dd),
+// so all workgroups get the identical value. Stream order makes the
+// producer's plain stores visible; no atomics, no write-through. Uniform
+// control flow. lds: 8 T.
+template <typename T>
+__device__ __forceinline__ Dd<T> sum_parts_dd(const T *__restrict__ part, int np, T *lds) {
+  __shared__ T bc[2];
+  Dd<T> v(T(0));
+  for (int i = threadIdx.x; i < np; i += kBlock) v += load_part(part, i);
+  v = block_sum_dd(v, lds);
+  if (threadIdx.x == 0) {
+    bc[0] = v.hi;
+    bc[1] = v.lo;
+  }
+  __syncthreads();
+  return Dd<T>(bc[0], bc[1]);
+}
 template <typename T>
 __device__ __forceinline__ T sum_parts(const T *__restrict__ part, int np, T *lds) {
-  __shared__ T bc;
-  T v[1] = {T(0)};
-  for (int i = threadIdx.x; i < np; i += kBlock) v[0] += part[i];
-  block_sum<T, 1>(v, lds);
-  if (threadIdx.x == 0) bc = v[0];
-  __syncthreads();
-  return bc;
+  return sum_parts_dd(part, np, lds).value();
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS operations, not for
@@ -148,37 +193,51 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int kPartsPerThread = 2 * kMaxGrid / kBlock;  // split SpMV: 2 launches
 template <typename T>
 __device__ __forceinline__ void parts_load(const T *__restrict__ part, int np,
-                                           T (&pl)[kPartsPerThread]) {
+                                           Dd<T> (&pl)[kPartsPerThread]) {
 #pragma unroll
   for (int k = 0; k < kPartsPerThread; ++k)  // unconditional (np >= 1): exact vmcnt waits
-    pl[k] = part[min((int)threadIdx.x + k * kBlock, np - 1)];
+    pl[k] = load_part(part, min((int)threadIdx.x + k * kBlock, np - 1));
 }
 // parts_load for a kernel with no stream loads behind it: only the np
 // partials are loaded (a few at small grids; parts_load issues
 // kPartsPerThread per thread whatever np is)
 template <typename T>
 __device__ __forceinline__ void parts_load_np(const T *__restrict__ part, int np,
-                                              T (&pl)[kPartsPerThread]) {
+                                              Dd<T> (&pl)[kPartsPerThread]) {
 #pragma unroll
   for (int k = 0; k < kPartsPerThread; ++k) {
     const int i = (int)threadIdx.x + k * kBlock;
-    pl[k] = i < np ? part[i] : T(0);
+    pl[k] = i < np ? load_part(part, i) : Dd<T>(T(0));
   }
 }
 template <typename T>
-__device__ __forceinline__ T parts_sum(const T (&pl)[kPartsPerThread], int np, T *lds) {
-  __shared__ T bc;
-  T v = T(0);
+__device__ __forceinline__ Dd<T> parts_sum_dd(const Dd<T> (&pl)[kPartsPerThread], int np,
+                                              T *lds) {
+  __shared__ T bc[2];
+  Dd<T> v(T(0));
 #pragma unroll
   for (int k = 0; k < kPartsPerThread; ++k)
     if ((int)threadIdx.x + k * kBlock < np) v += pl[k];  // sum_parts order
-  v = wave_sum(v);
+  v = wave_sum_dd(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) lds[w] = v;
+  if (lane == 0) {
+    lds[2 * w] = v.hi;
+    lds[2 * w + 1] = v.lo;
+  }
   lds_barrier();
-  if (threadIdx.x == 0) bc = ((lds[0] + lds[1]) + lds[2]) + lds[3];
+  if (threadIdx.x == 0) {
+    v = Dd<T>(lds[0], lds[1]);
+#pragma unroll
+    for (int k = 1; k < kBlock / 64; ++k) v += Dd<T>(lds[2 * k], lds[2 * k + 1]);
+    bc[0] = v.hi;
+    bc[1] = v.lo;
+  }
   lds_barrier();
-  return bc;
+  return Dd<T>(bc[0], bc[1]);
+}
+template <typename T>
+__device__ __forceinline__ T parts_sum(const Dd<T> (&pl)[kPartsPerThread], int np, T *lds) {
+  return parts_sum_dd(pl, np, lds).value();
 }
 
 // Late active check (measured in round 2):
@@ -195,6 +254,9 @@ template <typename T> __device__ __forceinline__ void keep(const T &a) {
   } else {
     asm volatile("" ::"v"(a));
   }
+}
+template <typename T> __device__ __forceinline__ void keep(const Dd<T> &a) {
+  asm volatile("" ::"v"(a.hi), "v"(a.lo));
 }
 template <typename T, int K> __device__ __forceinline__ void keep(const T (&a)[K]) {
 #pragma unroll
@@ -257,6 +319,53 @@ __device__ __forceinline__ bool grid_reduce(T (&v)[K], RedWs<T> *ws, T *lds, int
   return true;
 }
 
+// grid_reduce of one double-length pair (the loop's dots: k_cg_init's r.r,
+// the fused mode's p.Ap and r.r): the same tickets and order, pairs in
+// partials[i] / partials[kMaxGrid + i] and gsum[g] / gsum[kRedGroups + g].
+// True in the final workgroup, whose thread 0 then holds the total in v.
+template <typename T>
+__device__ __forceinline__ bool grid_reduce_dd(Dd<T> &v, RedWs<T> *ws, T *lds, int *flag) {
+  v = block_sum_dd(v, lds);
+  const unsigned G = gridDim.x;
+  const unsigned g = blockIdx.x % kRedGroups;
+  const unsigned ngroups = G < (unsigned)kRedGroups ? G : (unsigned)kRedGroups;
+  const unsigned members = (G - g + kRedGroups - 1) / kRedGroups;
+  if (threadIdx.x == 0) {
+    store_sc1(&ws->partials[blockIdx.x], v.hi);
+    store_sc1(&ws->partials[kMaxGrid + blockIdx.x], v.lo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&ws->ticket[g], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (prev == members - 1);
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  Dd<T> acc(T(0));
+  for (unsigned i = g + kRedGroups * threadIdx.x; i < G; i += kRedGroups * kBlock)
+    acc += Dd<T>(load_sc1(&ws->partials[i]), load_sc1(&ws->partials[kMaxGrid + i]));
+  acc = block_sum_dd(acc, lds);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&ws->ticket[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    store_sc1(&ws->gsum[g], acc.hi);
+    store_sc1(&ws->gsum[kRedGroups + g], acc.lo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&ws->top, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (prev == ngroups - 1);
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  if (threadIdx.x == 0) {
+    Dd<T> t(T(0));
+    for (unsigned q = 0; q < ngroups; ++q)
+      t += Dd<T>(load_sc1(&ws->gsum[q]), load_sc1(&ws->gsum[kRedGroups + q]));
+    v = t;
+    __hip_atomic_store(&ws->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
 // XCD-grouped logical workgroup id: blocks b and b+8 share an XCD (observed
 // dispatch, speed only — MI355X guide §Workgroup dispatch), so give each
 // blockIdx%8 group a contiguous range of logical ids.
@@ -314,6 +423,8 @@ struct CsrArgs {
   // CSR-stream block visit order (cgx_abi.cpp build_block_order): walk
   // position -> row block, a permutation within each XCD eighth (null: natural)
   const int *__restrict__ rbo;
+  // the interleaved val / col copy (kIL)
+  const char *__restrict__ il;
 };
 
 // the row block at walk position `pos` of the CSR-stream forms
@@ -686,6 +797,23 @@ __device__ __forceinline__ void spmv_rows_pipe(const CsrArgs &A, const T *__rest
     const bool ok = kk1 > kk0;  // empty blocks read pairs [0, 1] (nnz >= 2)
     const int ka = ok ? (kk0 & ~1) : 0;
     const int np = ok ? ((kk1 - ka + 1) >> 1) : 1;
+    if constexpr ((V & kIL) != 0) {
+      // pair P of the matrix (entries 2P, 2P + 1): chunk P / kIlCh holds
+      // kIlCh value pairs, then kIlCh column pairs (the same pairs, loads and
+      // values as below, from one array)
+      constexpr int64_t CB = (int64_t)kIlCh * (sizeof(PV) + sizeof(Int2));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = min(t + u * kBlock, np - 1);
+        const unsigned P = (unsigned)(ka >> 1) + (unsigned)j;
+        const char *cb = A.il + (int64_t)(P >> kIlLog) * CB;
+        const unsigned w = P & (kIlCh - 1);
+        vv[u] = ldg<NT>(reinterpret_cast<const PV *>(cb) + w);
+        cc[u] = tail_cols(ldg<NT>(reinterpret_cast<const Int2 *>(cb + kIlCh * sizeof(PV)) + w),
+                          ka + 2 * j, kk1);
+      }
+      return;
+    }
     const PV *v2 = reinterpret_cast<const PV *>(val + ka);
     const Int2 *c2 = reinterpret_cast<const Int2 *>(A.col + ka);
 #pragma unroll
@@ -1928,7 +2056,7 @@ template <class G> struct PfRaw<G, true> {
 template <typename T> struct TeamLds {
   typename PairU<T>::V pub[2][kTeamWaves][64];  // published centers, double-buffered by step
   SellLds<T> sell;                              // the per-slice form's dictionary, reductions
-  T red[kTeamWaves];
+  T red[2 * kTeamWaves];
 };
 
 // PF: the +-D pair a step ahead of the one the sums use is loaded (raw, in
@@ -2103,28 +2231,40 @@ __device__ __forceinline__ void spmv_lean_team(const CsrArgs &A, const Gather &x
   }
 }
 
-// the team's fixed-order sum of one value per thread (valid in thread 0)
-template <typename T> __device__ __forceinline__ T team_sum(T v, T *red) {
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+// the team's fixed-order sum of one pair per thread (valid in thread 0;
+// red: 2 T per wave)
+template <typename T> __device__ __forceinline__ Dd<T> team_sum(Dd<T> v, T *red) {
+  v = wave_sum_dd(v);
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * (threadIdx.x >> 6)] = v.hi;
+    red[2 * (threadIdx.x >> 6) + 1] = v.lo;
+  }
   __syncthreads();
-  T s = T(0);
+  Dd<T> s(T(0));
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int i = 0; i < kTeamWaves; ++i) s = s + red[i];
+    for (int i = 0; i < kTeamWaves; ++i) s += Dd<T>(red[2 * i], red[2 * i + 1]);
   return s;
 }
 // sum_parts's value (its order: threads 0..255 as a 256-thread workgroup)
 // in a team workgroup
 template <typename T> __device__ __forceinline__ T team_sum_parts(const T *part, int np, T *red) {
   __shared__ T bc;
-  T v = T(0);
+  Dd<T> v(T(0));
   if (threadIdx.x < kBlock)
-    for (int i = threadIdx.x; i < np; i += kBlock) v += part[i];
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0 && threadIdx.x < kBlock) red[threadIdx.x >> 6] = v;
+    for (int i = threadIdx.x; i < np; i += kBlock) v += load_part(part, i);
+  v = wave_sum_dd(v);
+  if ((threadIdx.x & 63) == 0 && threadIdx.x < kBlock) {
+    red[2 * (threadIdx.x >> 6)] = v.hi;
+    red[2 * (threadIdx.x >> 6) + 1] = v.lo;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) bc = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) {
+    v = Dd<T>(red[0], red[1]);
+#pragma unroll
+    for (int k = 1; k < kBlock / 64; ++k) v += Dd<T>(red[2 * k], red[2 * k + 1]);
+    bc = v.value();
+  }
   __syncthreads();
   return bc;
 }
@@ -2161,7 +2301,8 @@ __device__ __forceinline__ void spmv_any(const CsrArgs &A, const T *__restrict__
 template <typename T> struct EpiDot {  // helper = A p; value2 += helper.p
   T *__restrict__ Ap;
   const T *__restrict__ p;
-  T acc, pv, pv1;
+  Dd<T> acc;  // p.Ap (double-length)
+  T pv, pv1;
   __device__ __forceinline__ void pre(int i) { pv = p[i]; }
   __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
     pv = c0;
@@ -2201,7 +2342,8 @@ template <typename T> struct EpiInit {  // CG.hpp:325-331 (+ :341)
   const T *__restrict__ b;
   T *__restrict__ r;
   T *__restrict__ p;
-  T acc, bv, bv1;
+  Dd<T> acc;  // r.r (double-length)
+  T bv, bv1;
   __device__ __forceinline__ void pre(int i) { bv = b[i]; }
   __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
   __device__ __forceinline__ void row(int i, T s) {
@@ -2235,7 +2377,8 @@ template <typename T> struct EpiFused {
   T *__restrict__ Ap;
   T alpha, beta;
   bool do_x;
-  T acc, rv, pv, xv, rv1, pv1, xv1;
+  Dd<T> acc;  // p.Ap (double-length)
+  T rv, pv, xv, rv1, pv1, xv1;
   __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
   __device__ __forceinline__ void pre(int i) {
     rv = r[i];
@@ -2275,7 +2418,8 @@ template <typename T, bool NTP = false, bool NTS = false> struct EpiFD {
   T *__restrict__ Ap;
   T *__restrict__ pc;
   GatherP<T, NTP> g;
-  T acc, pv, pv1;
+  Dd<T> acc;  // p.Ap (double-length)
+  T pv, pv1;
   __device__ __forceinline__ void pre(int i) { pv = g(i); }
   __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
     pv = c0;
@@ -2363,9 +2507,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CsrArgs A, const T *__restri
   __shared__ LdsOf<T, V> sm;
   EpiInit<T> e{b, r, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{x}, e, sm);
-  T v[1] = {e.acc};
-  if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
-    st->rxr[0] = v[0];
+  Dd<T> v = e.acc;
+  if (grid_reduce_dd(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
+    st->rxr[0] = v.value();
+    ws->rr_part[0] = v.hi;  // the pair, for a partitioned run's all-reduce
+    ws->rr_part[1] = v.lo;
     st->pAp[0] = st->rr[0] = T(0);
     st->tol = tol;
     st->active[0] = 1;
@@ -2407,9 +2553,7 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot(CsrArgs A,
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
   // this workgroup's share of p.Ap; k_update_r sums the partials
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x, e.acc, sm.red);
 }
 
 // k_spmv_dot in the lean stencil walk (kVL): the same epilogue and partials
@@ -2438,9 +2582,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean(CsrArgs A, const T *__rest
   }
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x - A.wg0, e.acc, sm.red);
 }
 
 // The interior SpMV of a partitioned SELL matrix with the device peer
@@ -2461,9 +2603,7 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_push(
   __shared__ LdsOf<T, V> sm;
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherX<T>{p}, e, sm);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x - A.wg0, e.acc, sm.red);
 }
 
 // A partitioned matrix's interior slices by the lean walk (its layout skips
@@ -2488,9 +2628,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean_push(CsrArgs A, const T *_
   }
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x - A.wg0, e.acc, sm.red);
 }
 
 // The boundary slices with the peer transport's wait folded in (round 3;
@@ -2515,9 +2653,7 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_dot_bnd(
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherXL<T>{p, reinterpret_cast<const T *>(P.land_local), (int)A.n}, e,
                  sm);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x, e.acc, sm.red);
 }
 
 // Fused deferred-x iteration (mode 4), kernel 1 of 2 for body k in slot s
@@ -2565,9 +2701,7 @@ __global__ __launch_bounds__(kBlock, FdWaves<V>::w) void k_spmv_fd(
   const GatherP<T, NTP> g{r, pold, beta};
   EpiFD<T, NTP> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, g, e, sm);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x, e.acc, sm.red);
 }
 
 // k_spmv_fd in the lean stencil walk (kVL): the gathers form p_k = r +
@@ -2613,9 +2747,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean(
   const GatherP<T> g{r, pold, beta};
   EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_lean<T>(A, g, e, vd, vt);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x, e.acc, sm.red);
 }
 
 // k_spmv_fd_lean in the team form (CsrDev::vl_team): the published centers
@@ -2661,8 +2793,11 @@ __global__ __launch_bounds__(kTeamBlock) void k_spmv_fd_lean_t(
   const GatherP<T> g{r, pold, beta};
   EpiFD<T, false, NTS> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_lean_team<T, EpiFD<T, false, NTS>, GatherP<T>, PF>(A, g, e, vd, vt, tl);
-  const T v = team_sum(e.acc, tl.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v;
+  const Dd<T> v = team_sum(e.acc, tl.red);
+  if (threadIdx.x == 0) {
+    ws->pap_part[2 * (A.part_off + blockIdx.x)] = v.hi;
+    ws->pap_part[2 * (A.part_off + blockIdx.x) + 1] = v.lo;
+  }
 }
 
 // Mode 4 on a partitioned matrix (device peer transport), kernel 1 of 3:
@@ -2698,9 +2833,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fd_lean_push(
   }
   EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_lean<T>(A, g, e, vd, vt);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x - A.wg0] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x - A.wg0, e.acc, sm.red);
 }
 
 // Mode 4 on a partitioned matrix, kernel 2 of 3: the boundary rows as
@@ -2726,9 +2859,7 @@ __global__ __launch_bounds__(kBlock, SpmvWaves<V>::w) void k_spmv_fd_bnd(
   EpiFD<T> e{Ap, pc, g, T(0), T(0), T(0)};
   spmv_any<T, V>(A, val, GatherPL<T>{g, reinterpret_cast<const T *>(P.land_local), (int)A.n}, e,
                  sm);
-  T v[1] = {e.acc};
-  block_sum<T, 1>(v, sm.red);
-  if (threadIdx.x == 0) ws->pap_part[A.part_off + blockIdx.x] = v[0];
+  store_part(ws->pap_part, A.part_off + blockIdx.x, e.acc, sm.red);
 }
 
 // The final r.r of a mode-4 run that ended on an active body (no kernel 1
@@ -2764,20 +2895,20 @@ __global__ __launch_bounds__(kBlock) void k_spmv_fused(CsrArgs A, const T *__res
   if (!act && !xp) return;
   __shared__ LdsOf<T, V> sm;
   const T alpha = xp ? st->rxr[prev] / st->pAp[prev] : T(0);
-  T v[1] = {T(0)};
+  Dd<T> v(T(0));
   if (act) {
     const T beta = st->bodies == 0 ? T(0) : st->rr[prev] / st->rxr[prev];
     EpiFused<T> e{r, pp, pc, x, Ap, alpha, beta, xp, T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
     spmv_any<T, V>(A, val, GatherP<T>{r, pp, beta}, e, sm);
-    v[0] = e.acc;
+    v = e.acc;
   } else {
     // stopped after body k-1: only its deferred x update remains
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < A.n; i += stride)
       x[i] = x[i] + alpha * pp[i];
   }
-  if (grid_reduce<T, 1>(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
-    if (act) st->pAp[slot] = v[0];
+  if (grid_reduce_dd(v, ws, sm.red, &sm.flag) && threadIdx.x == 0) {
+    if (act) st->pAp[slot] = v.value();
     if (xp) st->xpend[prev] = 0;
   }
 }
@@ -2788,7 +2919,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_x(int64_t n, T *__restrict__ x
                                                     const T *__restrict__ p, CgScalars<T> *st,
                                                     int slot, RedWs<T> *ws) {
   if (!st->xpend[slot]) return;
-  __shared__ T red[4];
+  __shared__ T red[8];
   __shared__ int flag;
   const T alpha = st->rxr[slot] / st->pAp[slot];
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -2911,7 +3042,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // recorded) and marks the body's x update pending (ran[slot])
   const auto *cst = (const __attribute__((address_space(4))) CgScalars<T> *)st;
   const bool act = cst->active[slot] != 0;  // branched on after the first loads
-  __shared__ T red[4];
+  __shared__ T red[8];
   __shared__ int flag;
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
@@ -2929,7 +3060,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // make its wait drain the prefetch too
   const T rxr = cst->rxr[slot];
   const T pAp_st = cst->pAp[slot];
-  T pl[kPartsPerThread];
+  Dd<T> pl[kPartsPerThread];
   const bool from_parts = !FUSED && np_pap > 0;
   if (from_parts) parts_load(ws->pap_part, np_pap, pl);
   V rv[kUR], av[kUR];
@@ -2963,7 +3094,8 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     }
     return;
   }
-  T pAp = from_parts ? parts_sum(pl, np_pap, red) : pAp_st;
+  const Dd<T> pd = from_parts ? parts_sum_dd(pl, np_pap, red) : Dd<T>(pAp_st);
+  T pAp = pd.value();
   // (PEER without partials: the one-waiter form's k_peer_allreduce has put
   // the world p.Ap into st already)
   if (PEER && from_parts) {
@@ -2973,8 +3105,8 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
       peer_fault(st, slot, P);
       return;
     }
-    if (!peerdev::world_sum((double)pAp, P->state->arb[slot & 1] + 1, *P,
-                            &wres, &wok)) {
+    if (!peerdev::world_sum(Dd<double>((double)pd.hi, (double)pd.lo),
+                            P->state->arb[slot & 1] + 1, *P, &wres, &wok)) {
       peer_fault(st, slot, P);
       return;
     }
@@ -2995,7 +3127,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
       st->ran[slot] = 1;
     }
   }
-  T acc = T(0);
+  Dd<T> acc(T(0));  // r.r (double-length)
   for (bool first = true; i + (kUR - 1) * stride < n2; i += kUR * stride, first = false) {
     if (!first) {
 #pragma unroll
@@ -3032,19 +3164,22 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
     guse[3] = true;
     flush_group_range<T>(n, xf->x, xf->P[0], xf->P[1], xf->P[2], xf->P[3], ga, guse, rev);
   }
-  T v[1] = {acc};
+  Dd<T> v = acc;
   if constexpr (!FUSED) {  // this workgroup's share of r.r; the next kernel sums them
-    block_sum<T, 1>(v, red);
+    v = block_sum_dd(v, red);
     if (threadIdx.x == 0) {
-      if (PEER && rule)  // ... or this kernel's last workgroup (k_update_r_peer_rule)
-        store_sc1(&ws->rr_part[blockIdx.x], v[0]);
-      else
-        ws->rr_part[blockIdx.x] = v[0];
+      if (PEER && rule) {  // ... or this kernel's last workgroup (k_update_r_peer_rule)
+        store_sc1(&ws->rr_part[2 * blockIdx.x], v.hi);
+        store_sc1(&ws->rr_part[2 * blockIdx.x + 1], v.lo);
+      } else {
+        ws->rr_part[2 * blockIdx.x] = v.hi;
+        ws->rr_part[2 * blockIdx.x + 1] = v.lo;
+      }
     }
     return;
   }
-  if (grid_reduce<T, 1>(v, ws, red, &flag) && threadIdx.x == 0) {
-    st->rr[slot] = v[0];
+  if (grid_reduce_dd(v, ws, red, &flag) && threadIdx.x == 0) {
+    st->rr[slot] = v.value();
     if (FUSED) {
       const int nxt = (slot + 1) & 3;
       const T rxr = st->rxr[slot];
@@ -3053,7 +3188,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
       const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
       const bool cont = !cond && m < st->cap;
       st->active[nxt] = cont ? 1 : 0;
-      st->rxr[nxt] = v[0];
+      st->rxr[nxt] = st->rr[slot];
       st->xpend[slot] = 1;
       st->stopped = cond ? 1 : (cont ? 0 : 2);
     }
@@ -3147,17 +3282,21 @@ __global__ __launch_bounds__(kBlock) void k_update_r_peer_rule(int64_t n, T *r,
   if (!st->active[slot] ||
       __hip_atomic_load(&P.state->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     return;
-  __shared__ T red[4];
-  __shared__ T bc;
-  T v[1] = {T(0)};
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += kBlock) v[0] += load_sc1(&ws->rr_part[i]);
-  block_sum<T, 1>(v, red);
-  if (threadIdx.x == 0) bc = v[0];
+  __shared__ T red[8];
+  __shared__ T bc[2];
+  Dd<T> v(T(0));
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += kBlock)
+    v += Dd<T>(load_sc1(&ws->rr_part[2 * i]), load_sc1(&ws->rr_part[2 * i + 1]));
+  v = block_sum_dd(v, red);
+  if (threadIdx.x == 0) {
+    bc[0] = v.hi;
+    bc[1] = v.lo;
+  }
   __syncthreads();
   const unsigned long long t = P.state->arb[slot & 1] + 2;
   __shared__ double wres;
   __shared__ int wok;
-  const bool ok = peerdev::world_sum((double)bc, t, P, &wres, &wok);
+  const bool ok = peerdev::world_sum(Dd<double>((double)bc[0], (double)bc[1]), t, P, &wres, &wok);
   if (threadIdx.x == 0) {
     if (!ok) {
       P.state->fault = 1;
@@ -3183,10 +3322,11 @@ __device__ __forceinline__ void update_xp_body(int64_t n, T *__restrict__ x, T *
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
   }
-  __shared__ T red[4];
+  __shared__ T red[8];
   const T rxr = st->rxr[slot];
   const T alpha = rxr / st->pAp[slot];
-  T rr = np_rr > 0 ? sum_parts(ws->rr_part, np_rr, red) : st->rr[slot];
+  const Dd<T> rd = np_rr > 0 ? sum_parts_dd(ws->rr_part, np_rr, red) : Dd<T>(st->rr[slot]);
+  T rr = rd.value();
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
@@ -3194,7 +3334,7 @@ __device__ __forceinline__ void update_xp_body(int64_t n, T *__restrict__ x, T *
       peer_fault(st, slot, P);
       return;
     }
-    if (!peerdev::world_sum((double)rr, P->state->arb[slot & 1] + 2, *P, &wres,
+    if (!peerdev::world_sum(Dd<double>((double)rd.hi, (double)rd.lo), P->state->arb[slot & 1] + 2, *P, &wres,
                             &wok)) {
       peer_fault(st, slot, P);
       return;
@@ -3282,7 +3422,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_dot_acc(int64_t n, const T *__restrict__ x,
                                                     const T *__restrict__ y, T *res,
                                                     RedWs<T> *ws) {
-  __shared__ T red[4];
+  __shared__ T red[8];
   __shared__ int flag;
   T acc = T(0);
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -3626,6 +3766,7 @@ inline CsrArgs args(const CsrDev &A) {
   }
   a.col16 = A.col16;
   a.rbo = A.rbo;
+  a.il = A.il;
   if (vl_active(A)) {
     a.vl_cls = A.vl_cls;
     a.vl_tab = A.vl_tab;
@@ -3704,7 +3845,7 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
   const bool act = cst->active[slot] != 0;
   const T rxr = cst->rxr[slot];
   const T rr_st = cst->rr[slot];
-  T pl[kPartsPerThread];
+  Dd<T> pl[kPartsPerThread];
   if (np_rr > 0) parts_load_np(ws->rr_part, np_rr, pl);
   using V = typename Vec2<T>::V;
   const int64_t n2 = n >> 1;
@@ -3734,8 +3875,9 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
     if (blockIdx.x == 0 && threadIdx.x == 0) st->active[nxt] = 0;
     return;
   }
-  __shared__ T red[4];
-  T rr = np_rr > 0 ? parts_sum(pl, np_rr, red) : rr_st;
+  __shared__ T red[8];
+  const Dd<T> rd = np_rr > 0 ? parts_sum_dd(pl, np_rr, red) : Dd<T>(rr_st);
+  T rr = rd.value();
   if constexpr (PEER) {  // r.r all-reduced here (tag base + 2)
     __shared__ double wres;
     __shared__ int wok;
@@ -3743,7 +3885,7 @@ __device__ __forceinline__ void update_p_defer_body(int64_t n, T *__restrict__ x
       peer_fault(st, slot, PD);
       return;
     }
-    if (!peerdev::world_sum((double)rr, PD->state->arb[slot & 1] + 2, *PD,
+    if (!peerdev::world_sum(Dd<double>((double)rd.hi, (double)rd.lo), PD->state->arb[slot & 1] + 2, *PD,
                             &wres, &wok)) {
       peer_fault(st, slot, PD);
       return;
@@ -3928,7 +4070,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_group(int64_t n, T *__restrict
 // dot before its RCCL all-reduce)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_finalize(const T *__restrict__ part, int np, T *dst) {
-  __shared__ T red[4];
+  __shared__ T red[8];
   const T v = sum_parts(part, np, red);
   if (threadIdx.x == 0) *dst = v;
 }
@@ -3974,7 +4116,10 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
   // retired half-tile (64), three-stage (128) and wave-tile (512) bits drop
   // (a schedule built for smaller tiles fits the full-tile kernels)
   const bool c16 = (v & kC16) && A.col16 && (v & 4) && !(v & (8 | 256));
+  // the interleaved copy: the pipelined paired loop only (13 | kIL, 15 | kIL)
+  const bool il = (v & kIL) && A.il && (v & 12) == 12 && !(v & (256 | kC16)) && A.nnz >= 2;
   v &= 1023 & ~(64 | 128 | 512);
+  if (il) return v | kIL;
   if (((uintptr_t)A.val % (2 * sizeof(T))) || ((uintptr_t)A.col % 8) || A.nnz < 2)
     return 0;  // plain loads, no pipelining (any schedule with <= 2042-entry blocks)
   if (c16) return v | kC16;  // 132..135: paired loop, 16-bit column deltas
@@ -4022,6 +4167,8 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
     case 266: CGX_LAUNCH_V(KERNEL, 266, __VA_ARGS__);          \
     case 267: CGX_LAUNCH_V(KERNEL, 267, __VA_ARGS__);          \
     case 133: CGX_LAUNCH_V(KERNEL, 133, __VA_ARGS__);          \
+    case 67108877: CGX_LAUNCH_V(KERNEL, 67108877, __VA_ARGS__);\
+    case 67108879: CGX_LAUNCH_V(KERNEL, 67108879, __VA_ARGS__);\
     case 135: CGX_LAUNCH_V(KERNEL, 135, __VA_ARGS__);          \
     case 2048: CGX_LAUNCH_V(KERNEL, 2048, __VA_ARGS__);        \
     case 2050: CGX_LAUNCH_V(KERNEL, 2050, __VA_ARGS__);        \
@@ -4069,7 +4216,7 @@ template <typename T> inline int spmv_variant(const CsrDev &A, int v = kSpmvV) {
 // 8% of the value-code kernel at 256^3 (tools/gpu_vc_ab.sh).
 #define CGX_SPMV_LIST(X)                                                                    \
   X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(12) X(13) X(14) X(15) X(264) X(265) X(266)      \
-  X(133) X(135)                                                                             \
+  X(133) X(135) X(67108877) X(67108879)                                                     \
   X(267) X(2048) X(2050) X(2056) X(2058) X(6144) X(6146) X(8192) X(8194) X(24576) X(24578)  \
   X(40960) X(40962) X(303104) X(303106) X(565248) X(565250) X(827392) X(827394) X(1613824)  \
   X(1613826) X(1875968) X(1875970) X(3710976) X(3710978) X(3973120) X(3973122)              \
@@ -4226,6 +4373,8 @@ hipError_t Launch<T>::spmv_dot_variant(int v, const CsrDev &A, const T *p, T *Ap
     case 31: CGX_LAUNCH_V(k_spmv_dot, 31, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 47: CGX_LAUNCH_V(k_spmv_dot, 47, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     case 63: CGX_LAUNCH_V(k_spmv_dot, 63, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 67108927: CGX_LAUNCH_V(k_spmv_dot, 67108927, args(A), (const T *)A.val, p, Ap, st, 0, ws);
+    case 67108911: CGX_LAUNCH_V(k_spmv_dot, 67108911, args(A), (const T *)A.val, p, Ap, st, 0, ws);
     default: break;
   }
   CGX_SPMV_SWITCH(vv, k_spmv_dot, args(A), (const T *)A.val, p, Ap, st, 0, ws);
@@ -4745,6 +4894,44 @@ hipError_t col16_build(const CsrDev &A, short *col16, unsigned *bad, hipStream_t
   const int grid = A.nrb < kMaxGrid ? A.nrb : kMaxGrid;
   CGX_GGL(k_col16, dim3(grid), dim3(kBlock), 0, s, A.rb, A.rbk, A.col, A.nrb, col16,
                      bad);
+  return hipGetLastError();
+}
+
+// The interleaved val / col copy (kIL): pair P (entries 2P, 2P + 1; past
+// nnz: 0) into chunk P / kIlCh, values first, then columns
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_il_pack(int64_t nnz, int64_t pairs,
+                                                    const T *__restrict__ val,
+                                                    const int *__restrict__ col, char *il) {
+  using PV = typename PairOf<T>::V;
+  constexpr int64_t CB = (int64_t)kIlCh * (sizeof(PV) + sizeof(Int2));
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t P = (int64_t)blockIdx.x * kBlock + threadIdx.x; P < pairs; P += stride) {
+    const int64_t e = 2 * P;
+    PV v;
+    Int2 c;
+    v.x = val[e];
+    c.x = col[e];
+    v.y = e + 1 < nnz ? val[e + 1] : T(0);
+    c.y = e + 1 < nnz ? col[e + 1] : 0;
+    char *cb = il + (P >> kIlLog) * CB;
+    reinterpret_cast<PV *>(cb)[P & (kIlCh - 1)] = v;
+    reinterpret_cast<Int2 *>(cb + kIlCh * sizeof(PV))[P & (kIlCh - 1)] = c;
+  }
+}
+
+hipError_t il_build(const CsrDev &A, int es, char *il, hipStream_t s) {
+  if (A.nnz < 2) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(il, 0, (size_t)il_bytes(A.nnz, es), s);
+  if (e != hipSuccess) return e;
+  const int64_t pairs = (A.nnz + 1) / 2;
+  const int grid = elem_grid(pairs, 4);
+  if (es == 8)
+    CGX_GGL(k_il_pack<double>, dim3(grid), dim3(kBlock), 0, s, A.nnz, pairs,
+            (const double *)A.val, A.col, il);
+  else
+    CGX_GGL(k_il_pack<float>, dim3(grid), dim3(kBlock), 0, s, A.nnz, pairs,
+            (const float *)A.val, A.col, il);
   return hipGetLastError();
 }
 

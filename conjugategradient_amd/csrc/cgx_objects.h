@@ -94,10 +94,11 @@ struct PeerDev {  // kernel argument (by value)
   int nopoll;
   int pad_;
 };
-// mailbox layout inside a rank's ctl allocation: val[2][kPeerMax] doubles,
-// tag[2][kPeerMax] u64 (parity = tag & 1), then flag[kPeerMax][kPushWG] u64
-constexpr int kPeerTagOff = 2 * kPeerMax * 8;
-constexpr int kPeerFlagOff = 4 * kPeerMax * 8;
+// mailbox layout inside a rank's ctl allocation: val[2][kPeerMax] double-
+// length pairs (hi, lo), tag[2][kPeerMax] u64 (parity = tag & 1), then
+// flag[kPeerMax][kPushWG] u64
+constexpr int kPeerTagOff = 4 * kPeerMax * 8;
+constexpr int kPeerFlagOff = 6 * kPeerMax * 8;
 constexpr size_t kPeerCtlBytes = kPeerFlagOff + (size_t)kPeerMax * kPushWG * 8;
 struct Peer {
   bool on = false;
@@ -176,6 +177,7 @@ struct cgx_csr {
   void *d_sell_sl_t = nullptr, *d_vct = nullptr;       // value-code templates (kVT)
   int64_t vt_slices = 0;                               // slices that read a template
   void *d_col16 = nullptr;  // CSR-stream 16-bit column deltas (cgx::CsrDev::col16)
+  void *d_il = nullptr;     // CSR-stream interleaved val / col copy (cgx::CsrDev::il)
   void *d_rbo = nullptr;    // CSR-stream block visit order (cgx::CsrDev::rbo)
   // lean stencil walk (kVL, cgx_abi.cpp build_lean): per-slice classes in
   // slice order (host), their device layout for grid dev.vl_grid, the table

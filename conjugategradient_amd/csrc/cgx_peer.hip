@@ -100,22 +100,31 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_peer_allreduce(const T *__restrict__ part, int np,
                                                             T *dst, CgScalars<T> *st, int slot,
                                                             PeerDev P, int which) {
-  __shared__ double red[kBlock / 64];
+  __shared__ double red[2 * (kBlock / 64)];
   __shared__ int ok_s;
   if (skip_body(st, slot, P.state)) return;
-  double v = 0;
-  for (int k = threadIdx.x; k < np; k += kBlock) v += (double)part[k];
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  // this rank's double-length sum of its np partial pairs in sum_parts_dd's
+  // order (the fused form's value, bit for bit)
+  Dd<double> v(0.0);
+  for (int k = threadIdx.x; k < np; k += kBlock)
+    v += Dd<double>((double)part[2 * k], (double)part[2 * k + 1]);
+  v = wave_sum_dd(v);
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * (threadIdx.x >> 6)] = v.hi;
+    red[2 * (threadIdx.x >> 6) + 1] = v.lo;
+  }
   __syncthreads();
-  const double mine = ((red[0] + red[1]) + red[2]) + red[3];
+  Dd<double> mine(red[0], red[1]);
+  for (int w = 1; w < kBlock / 64; ++w) mine += Dd<double>(red[2 * w], red[2 * w + 1]);
   const unsigned long long tag = which ? P.state->arb[slot & 1] + which : P.state->ar + 1;
   const int par = (int)(tag & 1);
   if (threadIdx.x < 64) {
     bool ok = true;
     if ((int)threadIdx.x < P.world) {
       char *box = P.ctl[threadIdx.x];
-      st_sysd(reinterpret_cast<double *>(box) + par * kPeerMax + P.rank, mine);
+      double *val = reinterpret_cast<double *>(box) + 2 * (par * kPeerMax + P.rank);
+      st_sysd(val, mine.hi);
+      st_sysd(val + 1, mine.lo);
       __threadfence_system();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       st_sys(reinterpret_cast<unsigned long long *>(box + kPeerTagOff) + par * kPeerMax + P.rank,
@@ -133,10 +142,10 @@ __global__ __launch_bounds__(kBlock) void k_peer_allreduce(const T *__restrict__
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  const double *vals = reinterpret_cast<const double *>(P.ctl[P.rank]) + par * kPeerMax;
-  double s = 0;
-  for (int q = 0; q < P.world; ++q) s += ld_sysd(vals + q);
-  *dst = (T)s;
+  const double *vals = reinterpret_cast<const double *>(P.ctl[P.rank]) + 2 * par * kPeerMax;
+  Dd<double> s(0.0);
+  for (int q = 0; q < P.world; ++q) s += Dd<double>(ld_sysd(vals + 2 * q), ld_sysd(vals + 2 * q + 1));
+  *dst = (T)s.value();
   P.state->ar = tag;
   if (which == 0) P.state->arb[0] = P.state->arb[1] = tag;
   if (which == 2) P.state->arb[(slot + 1) & 1] = tag;
@@ -268,9 +277,10 @@ template <typename T> int self_test(cgx_csr *A, bool *ok) {
   if (!rc) rc = peer_wait<T>(A, v2, nullptr, 0, s);
   T want[3] = {T(0), T(0), T(0)};
   for (int r = 0; r < 3 && !rc; ++r) {
-    const T mine[2] = {(T)(ctx->rank + 1) * (T)(r + 1), (T)0.5};
+    // two partial pairs (hi, lo): (rank + 1) (r + 1) and 0.5
+    const T mine[4] = {(T)(ctx->rank + 1) * (T)(r + 1), T(0), (T)0.5, T(0)};
     for (int q = 0; q < ctx->world; ++q) want[r] += (T)(q + 1) * (T)(r + 1) + (T)0.5;
-    e = hipMemcpyAsync(part, mine, 2 * sizeof(T), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(part, mine, 4 * sizeof(T), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) rc = hip_fail(e, "peer self-test (copy)");
     if (!rc) rc = peer_allreduce<T>(A, part, 2, res + r, nullptr, 0, s, 0);
     if (!rc) {

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "cgx_dd.h"
 #include "cgx_objects.h"
 
 namespace cgx {
@@ -81,8 +82,8 @@ __device__ __forceinline__ bool wait_pushes(const PeerDev &P, unsigned long long
 // the spins never wait on a workgroup that is not yet resident (dispatch
 // order is undefined). Uniform control flow; thread 0's lds slots carry the
 // result. false: a spin timed out.
-__device__ __forceinline__ bool world_sum(double mine, unsigned long long t, const PeerDev &P,
-                                          double *res_lds, int *ok_lds) {
+__device__ __forceinline__ bool world_sum(Dd<double> mine, unsigned long long t,
+                                          const PeerDev &P, double *res_lds, int *ok_lds) {
   const int par = (int)(t & 1);
   if (threadIdx.x < 64) {
     int claim = 0;
@@ -95,7 +96,9 @@ __device__ __forceinline__ bool world_sum(double mine, unsigned long long t, con
     if ((int)threadIdx.x < P.world) {
       if (publisher) {
         char *box = P.ctl[threadIdx.x];
-        st_sysd(reinterpret_cast<double *>(box) + par * kPeerMax + P.rank, mine);
+        double *val = reinterpret_cast<double *>(box) + 2 * (par * kPeerMax + P.rank);
+        st_sysd(val, mine.hi);
+        st_sysd(val + 1, mine.lo);
         __threadfence_system();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_sys(reinterpret_cast<unsigned long long *>(box + kPeerTagOff) + par * kPeerMax +
@@ -110,10 +113,13 @@ __device__ __forceinline__ bool world_sum(double mine, unsigned long long t, con
       *ok_lds = ok;
       if (ok) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
-        const double *vals = reinterpret_cast<const double *>(P.ctl[P.rank]) + par * kPeerMax;
-        double s = 0;
-        for (int q = 0; q < P.world; ++q) s += ld_sysd(vals + q);
-        *res_lds = s;
+        // the ranks' pairs in rank order, rounded once: the world value no
+        // longer depends on how the rows were split between the ranks
+        const double *vals =
+            reinterpret_cast<const double *>(P.ctl[P.rank]) + 2 * par * kPeerMax;
+        Dd<double> s(0.0);
+        for (int q = 0; q < P.world; ++q) s += Dd<double>(ld_sysd(vals + 2 * q), ld_sysd(vals + 2 * q + 1));
+        *res_lds = s.value();
       }
     }
   }

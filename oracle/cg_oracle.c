@@ -431,3 +431,106 @@ int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
   free(helper); free(rnext); free(p);
   return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* The engine's dot model (round 6): the same iteration as                  */
+/* orc_cg_solve_omp, every dot a double-length sum                          */
+/* ------------------------------------------------------------------------ */
+
+/* The reference's dots (VectorOperations.hpp:287-309, CG.hpp:378-379,
+ * 406-407) are sycl::reduction sums in an order AdaptiveCpp chooses (parity
+ * unpinned, cg_oracle.h). The GPU engine sums them as unevaluated pairs
+ * hi + lo (TwoSum on every addition) and rounds once, so its value does not
+ * depend on how rows are split. Here the same model on the CPU: each OpenMP
+ * thread sums its static chunk as a pair, the pairs are combined in thread
+ * order, one rounding. Both are the exact sum of the rounded products to
+ * within ~n u^2 of the sum of their magnitudes, so their rounded values agree
+ * except when the exact sum lies that close to a rounding boundary; every
+ * other value of the iteration is rounded as in orc_cg_solve. This is a
+ * checker for the engine's arithmetic (x bit for bit), not a claim about the
+ * reference's summation order. */
+typedef struct { double hi, lo; } orc_dd;
+static inline void dd_add(orc_dd *s, double x) {
+  const double t = s->hi + x;
+  const double z = t - s->hi;
+  s->lo += (s->hi - (t - z)) + (x - z);
+  s->hi = t;
+}
+#define ORC_MAX_THREADS 256
+static double dot_dd(int64_t n, const double *a, const double *b) {
+  orc_dd part[ORC_MAX_THREADS];
+  int nt = 1;
+#pragma omp parallel
+  {
+    const int t = omp_get_thread_num();
+#pragma omp single
+    nt = omp_get_num_threads();
+    orc_dd s = {0.0, 0.0};
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < n; ++i) dd_add(&s, a[i] * b[i]);
+    if (t < ORC_MAX_THREADS) part[t] = s;
+  }
+  orc_dd s = part[0];
+  for (int t = 1; t < nt && t < ORC_MAX_THREADS; ++t) {
+    dd_add(&s, part[t].hi);
+    s.lo += part[t].lo;
+  }
+  return s.hi + s.lo;
+}
+
+int orc_cg_solve_dd(int64_t n, const int *rowptr, const int *col, const double *val,
+                    const double *b, double *x, int has_x0, double tol, int64_t max_iter,
+                    int threads, orc_cg_result *res) {
+  if (threads > ORC_MAX_THREADS) threads = ORC_MAX_THREADS;
+  omp_set_num_threads(threads > 0 ? threads : 1);
+  double *helper = (double *)malloc((size_t)n * sizeof(double));
+  double *rnext = (double *)malloc((size_t)n * sizeof(double));
+  double *p = (double *)malloc((size_t)n * sizeof(double));
+  if (!helper || !rnext || !p) { free(helper); free(rnext); free(p); return 3; }
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {                               /* :324-332 */
+    if (!has_x0) x[i] = 0;
+  }
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    double s = 0;
+    for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) s += val[j] * x[col[j]];
+    rnext[i] = b[i] - s;
+    p[i] = rnext[i];
+  }
+  double rxr = dot_dd(n, rnext, rnext);                           /* :341 */
+  if (res) res->rxr0 = rxr;
+  int64_t counter = 0, bodies = 0;
+  int done = 0;
+  do {
+    double alpha, beta;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {                             /* :374-375 */
+      double s = 0;
+      for (int j = rowptr[i]; j < rowptr[i + 1]; ++j) s += val[j] * p[col[j]];
+      helper[i] = s;
+    }
+    const double value2 = dot_dd(n, helper, p);                   /* :378-379 */
+    alpha = rxr / value2;                                         /* :385-386 */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      x[i] = x[i] + alpha * p[i];                                 /* :390 */
+      rnext[i] = rnext[i] - alpha * helper[i];                    /* :392-393 */
+    }
+    if (isnan(rxr) || sqrt(rxr) <= tol) done = 1;                 /* :400-403 */
+    const double value3 = dot_dd(n, rnext, rnext);                /* :406-407 */
+    beta = value3 / rxr;                                          /* :414 */
+    rxr = value3;                                                 /* :415 */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) p[i] = rnext[i] + beta * p[i];/* :418 */
+    ++bodies;
+    if (max_iter >= 0 && bodies >= max_iter) break;
+  } while ((uint64_t)(counter++) < (uint64_t)n && !done);        /* :436 */
+  if (res) {
+    res->iterations = bodies;
+    res->rxr = rxr;
+    res->stopped_by_tol = done;
+  }
+  free(helper); free(rnext); free(p);
+  return 0;
+}

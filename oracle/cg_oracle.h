@@ -102,6 +102,15 @@ int orc_cg_solve_omp(int64_t n, const int *rowptr, const int *col,
                      double tol, int64_t max_iter, int threads,
                      orc_cg_result *res);
 
+/* orc_cg_solve_omp with every dot a double-length sum (per-thread TwoSum
+ * pairs combined in thread order, one rounding): the GPU engine's dot model
+ * since round 6, whose value does not depend on how rows are split. A
+ * checker for the engine's arithmetic at full size (x bit for bit), not a
+ * statement about the reference's (unpinned) summation order. */
+int orc_cg_solve_dd(int64_t n, const int *rowptr, const int *col, const double *val,
+                    const double *b, double *x, int has_x0, double tol, int64_t max_iter,
+                    int threads, orc_cg_result *res);
+
 #ifdef __cplusplus
 }
 #endif

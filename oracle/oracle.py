@@ -73,6 +73,8 @@ def lib() -> C.CDLL:
         L.orc_cg_solve_omp.argtypes = [_i64] + [C.c_void_p] * 5 + [C.c_int, C.c_double, _i64,
                                                                    C.c_int, C.POINTER(CgResult)]
         L.orc_cg_solve_omp.restype = C.c_int
+        L.orc_cg_solve_dd.argtypes = L.orc_cg_solve_omp.argtypes
+        L.orc_cg_solve_dd.restype = C.c_int
         _lib = L
     return _lib
 
@@ -220,4 +222,17 @@ def cg_solve_omp(rowptr, col, val, b, tol: float, threads: int = 16, max_iter: i
                                 0 if x0 is None else 1, tol, max_iter, threads, C.byref(res))
     if rc:
         raise RuntimeError(f"orc_cg_solve_omp failed: {rc}")
+    return x, res
+
+
+def cg_solve_dd(rowptr, col, val, b, tol: float, threads: int = 16, max_iter: int = -1, x0=None):
+    """orc_cg_solve_dd: the iteration with double-length dots (the GPU
+    engine's dot model; x bit for bit against it). Returns (x, CgResult)."""
+    n = len(rowptr) - 1
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64, copy=True)
+    res = CgResult()
+    rc = lib().orc_cg_solve_dd(n, _ptr(rowptr), _ptr(col), _ptr(val), _ptr(b), _ptr(x),
+                               0 if x0 is None else 1, tol, max_iter, threads, C.byref(res))
+    if rc:
+        raise RuntimeError(f"orc_cg_solve_dd failed: {rc}")
     return x, res

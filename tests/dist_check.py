@@ -155,9 +155,14 @@ def main():
         xg = torch.cat([t[:c] for t, c in zip(xs, counts)]).numpy()
         rp, cl, vl = O.poisson(3, gxy, gxy, g)
         bg = np.arange(1, n + 1, dtype=np.float64)
+        dd_equal = None
         if a.bodies >= 0:
             _, xr = O.cg_fixed_iters_omp(rp, cl, vl, bg, a.bodies, 16)
             oracle_bodies = a.bodies
+            # the engine's dot model (double-length sums, round 6): x bit for
+            # bit whatever the split, where every all-reduce keeps the pairs
+            xdd, _ = O.cg_solve_dd(rp, cl, vl, bg, 0.0, threads=16, max_iter=a.bodies)
+            dd_equal = bool(np.array_equal(xg, xdd))
         else:
             xr, res = O.cg_solve(rp, cl, vl, bg, a.tol)
             oracle_bodies = res.iterations
@@ -175,6 +180,7 @@ def main():
                           "variant_lean_slices": [p[5] for p in parts],
                           "peer_form": [p[6] for p in parts],
                           "x_sha": hashlib.sha256(xg.tobytes()).hexdigest()[:16],
+                          "dd_equal": dd_equal,
                           "ok": ok}), flush=True)
     L.cgx_cg_destroy(cg)
     L.cgx_csr_destroy(A)

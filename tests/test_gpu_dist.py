@@ -68,6 +68,23 @@ def test_partitioned_solve_matches_oracle(nproc, transport, grid, mode):
         assert r["peer_form"] == [[nproc, 1]] * nproc, r["peer_form"]
 
 
+@pytest.mark.parametrize("nproc,transport", [(1, "rccl"), (2, "host-peer"), (4, "host-peer"),
+                                             (8, "host-peer")])
+def test_partitioned_x_independent_of_world_size(nproc, transport):
+    """The dots are double-length sums (round 6) from the threads through the
+    workgroup partials to the peer transport's world sum of the ranks' pairs
+    in rank order, rounded once: x after 30 bodies is bit for bit the dd
+    oracle's (oracle.cg_solve_dd) on 1 rank (RCCL at world size 1) and on 2,
+    4 and 8 ranks, in mode 3 and in mode 4 (lean interior)."""
+    for mode in (3, 4):
+        if mode == 4 and nproc == 1:
+            continue  # (the partitioned mode 4 needs the peer transport)
+        r = _run(nproc, transport, 64, mode, ["--nxy", "128", "--bodies", "30"], env=LEAN)
+        assert r["ok"], r
+        assert r["bodies"] == 30 and r["mode_run"] == mode
+        assert r["dd_equal"] is True, (nproc, mode, r["rel_err"])
+
+
 @pytest.mark.parametrize("transport,mode", [("host", 0), ("host-peer", 3), ("host-async", 3)])
 def test_eight_way_split(transport, mode):
     """Config 4's 8-way row split (BASELINE.json configs[3]) as 8 ranks on this

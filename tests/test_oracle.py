@@ -130,3 +130,19 @@ def test_cpu_baseline_matches_solver(oracle):
     xr, res = oracle.cg_solve(rp, cl, vl, b, 0.0, max_iter=30)
     assert res.iterations == 30 and t > 0
     assert rel(x, xr) < 1e-10
+
+
+def test_dd_oracle_independent_of_threads(oracle):
+    """oracle.cg_solve_dd (the engine's dot model: each dot a double-length
+    sum, rounded once): x after 30 bodies is bit for bit the same on 1, 3
+    and 8 OpenMP threads, on an irregular SPD matrix where the plain
+    OpenMP-reduction iteration moves with the thread count; and it stays
+    within the SURVEY §8(c) bar of the index-order restatement."""
+    from tests.util import irregular_spd, rel
+
+    rp, cl, vl = irregular_spd(60_000, mean_deg=3.83, seed=7)
+    b = np.arange(1, len(rp), dtype=np.float64)
+    xs = [oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=t, max_iter=30)[0] for t in (1, 3, 8)]
+    assert np.array_equal(xs[0], xs[1]) and np.array_equal(xs[0], xs[2])
+    xr, _ = oracle.cg_solve(rp, cl, vl, b, 0.0, max_iter=30)
+    assert rel(xs[0], xr) <= 1e-6

@@ -59,6 +59,8 @@ def main():
     for name in a.configs.split(","):
         A = matrix(q, name)
         n, nnz = A.N(), A.NNZ()
+        if any(v & 67108864 for v in variants):  # build the interleaved val / col copy (kIL)
+            check(L.cgx_csr_set_variant(A.schedule(), 67108879))
         # a second schedule with half tiles for the variants with bit 64
         half = C.c_void_p()
         check(L.cgx_csr_create(q.handle, n, nnz, A.rows().ptr, A.columns().ptr, A.data().ptr, 0,
