@@ -78,6 +78,8 @@ def update_bytes_per_iter(n: int, mode: int) -> int:
     +40 n), 34 n on average."""
     if mode == 4:  # the p update is folded into the SpMV (spmv_bytes_per_iter);
         return 24 * n + 12 * n  # the slot-3 x flush: x r/w + 4 p reads, once per 4 bodies
+    # mode 6: kernel 2 reads p (A p formed again) where update_r reads Ap: the
+    # same 24 n, plus its matrix stream (added by the caller)
     xp = 40 * n if mode in (1, 5) else 34 * n  # mode 5: priced as mode 1
     return 24 * n + xp
 
@@ -86,7 +88,7 @@ def spmv_bytes_per_iter(stream_bytes: int, n: int, mode: int) -> int:
     """The SpMV launch: its matrix stream (cgx_csr_stream_bytes) + p read + Ap
     written (16 n); mode 4's k_spmv_fd reads r and p_{k-1} and writes p_k and
     Ap (32 n)."""
-    return stream_bytes + (32 * n if mode == 4 else 16 * n)
+    return stream_bytes + (32 * n if mode == 4 else 8 * n if mode == 6 else 16 * n)
 
 
 def parse(argv=None):
@@ -116,7 +118,7 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
-    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4, 5], default=0,
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4, 5, 6], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
                          "2 fused (single GPU), 3 three kernels with the x update deferred, "
                          "4 two kernels (p update folded into the SpMV), x deferred")
@@ -578,6 +580,8 @@ def run(args) -> None:
     # compulsory bytes of one iteration in the streamed formats, all ranks
     spmv_fmt_local = spmv_bytes_per_iter(sbytes.value, n_local, mode_eff)
     iter_local = spmv_fmt_local + update_bytes_per_iter(n_local, mode_eff)
+    if mode_eff == 6:  # kernel 2's walk streams the matrix's format again
+        iter_local += sbytes.value
     if fused:
         iter_local = sbytes.value + 48 * n_local + 24 * n_local
     iter_global = iter_local
@@ -614,8 +618,8 @@ def run(args) -> None:
         ach = kb / (avg[1] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
             (16 * n_local if mode_eff == 4 else 0)
-        kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" + sfx if lean_on else "k_spmv_fd"}.get(
-            mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
+        kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" + sfx if lean_on else "k_spmv_fd",
+                 6: "k_spmv_lean_dot"}.get(mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname,
@@ -633,6 +637,9 @@ def run(args) -> None:
         if mode_eff == 4:  # every fourth k_update_r also applies the group's x updates
             roof["other_kernels_avg_us"] = {"k_update_r (+ x flush in 1 of 4)":
                                             round(avg[2] * 1e3, 2)}
+        elif mode_eff == 6:
+            roof["other_kernels_avg_us"] = {"k_spmv_lean_updr": round(avg[2] * 1e3, 2),
+                                            "k_update_p": round(avg[3] * 1e3, 2)}
         elif not fused:
             roof["other_kernels_avg_us"]["k_update_p"] = round(avg[3] * 1e3, 2)
         if world == 1 and not args.no_traffic:
@@ -710,7 +717,10 @@ def run(args) -> None:
                                          "2 kernels (p update in the SpMV), x update deferred "
                                          "over 4 bodies"),
                                      5: "persistent body (one launch per chunk of bodies, two "
-                                        "grid-wide exchanges per body)"}[mode_eff] +
+                                        "grid-wide exchanges per body)",
+                                     6: "3 kernels, Ap recomputed (the walk's p.Ap; the walk "
+                                        "again with r -= alpha A p; the p update), x update "
+                                        "deferred over 4 bodies"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
                        "setup": setup,
                        "spmv_variant": int(variant.value),

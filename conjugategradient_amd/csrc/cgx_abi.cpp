@@ -357,6 +357,21 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
   int npp = 0;
   const PeerDev *far = fused_ar(cg);
   const bool sep = A->dist && !far;  // a separate all-reduce step per dot
+  if (cg->recompute) {
+    // mode 6: kernel 1 keeps only p.Ap, kernel 2 forms A p again and updates
+    // r in the walk's epilogue (no Ap vector: 8 N bytes written and read
+    // less per body), kernel 3 as mode 3's (np_rr: kernel 2's grid)
+    if ((rc = timed(cg, 1, s, [&] { return Launch<T>::lean_dot(A->dev, p, st, slot, ws, s, par); })))
+      return rc;
+    if ((rc = timed(cg, 2, s, [&] {
+           return Launch<T>::lean_updr(A->dev, p, r, st, slot, ws, s, rpar);
+         })))
+      return rc;
+    return timed(cg, 3, s, [&] {
+      return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, A->dev.vl_grid, s,
+                                       par, nullptr);
+    });
+  }
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;
   if (sep && (rc = dist_dot<T>(cg, ws->pap_part, npp, &st->pAp[slot], slot, 1))) return rc;
   if ((rc = timed(cg, 2, s, [&] {
@@ -3035,9 +3050,11 @@ static bool coop_auto(const cgx_cg *cg) {
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
-  CGX_REQUIRE(mode >= 0 && mode <= 5, CGX_EINVAL,
+  CGX_REQUIRE(mode >= 0 && mode <= 6, CGX_EINVAL,
               "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
-              "4 fused with deferred x, 5 persistent body", mode);
+              "4 fused with deferred x, 5 persistent body, 6 recomputed Ap", mode);
+  CGX_REQUIRE(mode != 6 || (!cg->A->dist && vl_whole(cg->A->dev)), CGX_EUNSUPPORTED,
+              "mode 6 (recomputed Ap) needs the lean stencil walk on a single device");
   int coop_r = 0;
   if (!cg->begun) {  // mode 5's form and test hook
     cg->coop_stall = -1;
@@ -3095,8 +3112,10 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
       }
     }
   }
-  const bool f = mode == 2, d = mode == 3, fd = mode == 4, c = mode == 5;
-  if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop) {
+  const bool f = mode == 2, d = mode == 3 || mode == 6, fd = mode == 4, c = mode == 5;
+  const bool rc6 = mode == 6;
+  if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop ||
+      rc6 != cg->recompute) {
     CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
     drop_graph(cg);
   }
@@ -3140,6 +3159,7 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   cg->fused = f;
   cg->defer = d;
   cg->fdefer = fd;
+  cg->recompute = rc6;
   return CGX_OK;
 }
 
@@ -3157,7 +3177,7 @@ extern "C" int cgx_csr_fd_grid(cgx_csr *A, int *fd_grid, int *spmv_grid) {
 
 extern "C" int cgx_cg_get_mode(cgx_cg *cg, int *mode) {
   CGX_REQUIRE(cg && mode, CGX_EINVAL, "NULL argument");
-  *mode = cg->coop ? 5 : cg->fdefer ? 4 : cg->defer ? 3 : cg->fused ? 2 : 1;
+  *mode = cg->coop ? 5 : cg->fdefer ? 4 : cg->recompute ? 6 : cg->defer ? 3 : cg->fused ? 2 : 1;
   return CGX_OK;
 }
 

@@ -297,6 +297,13 @@ template <typename T> struct Launch {
                                   const T *p, T *Ap, CgScalars<T> *st, int slot, RedWs<T> *ws,
                                   hipStream_t s, const PeerDev *P);
   static int rows_grid(const CsrDev &A, int count);
+  // mode 6 (recomputed Ap; the whole-matrix lean walk only): kernel 1, the
+  // walk's p.Ap partials [0, vl_grid) with no Ap stored; kernel 2, alpha, the
+  // walk again with r -= alpha (A p) in its epilogue, r.r partials [0, vl_grid)
+  static hipError_t lean_dot(const CsrDev &A, const T *p, CgScalars<T> *st, int slot,
+                             RedWs<T> *ws, hipStream_t s, int rev);
+  static hipError_t lean_updr(const CsrDev &A, const T *p, T *r, CgScalars<T> *st, int slot,
+                              RedWs<T> *ws, hipStream_t s, int rev);
   // a partitioned matrix's interior slices by the lean walk (A.vl_split), the
   // halo push in the first wg0 workgroups when P is given; partials [0, vl_grid)
   static hipError_t spmv_lean_interior(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,

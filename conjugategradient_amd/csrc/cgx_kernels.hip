@@ -2469,6 +2469,70 @@ template <typename T, bool NTP = false, bool NTS = false> struct EpiFD {
     if (l1) acc += s1 * pv1;
   }
 };
+// Recomputed-Ap body (mode 6), kernel 1: value2 += helper.p (CG.hpp:378-
+// 379) with helper = A p not stored — kernel 2 forms it again.
+template <typename T> struct EpiDotOnly {
+  const T *__restrict__ p;
+  Dd<T> acc;  // p.Ap (double-length)
+  T pv, pv1;
+  __device__ __forceinline__ void pre(int i) { pv = p[i]; }
+  __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
+    pv = c0;
+    pv1 = c1;
+  }
+  __device__ __forceinline__ void row(int, T s) { acc += s * pv; }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    pv = p[i0];
+    pv1 = p[i1];
+  }
+  __device__ __forceinline__ void row2(int, T s0, T s1, bool l0, bool l1) {
+    if (l0) acc += s0 * pv;
+    if (l1) acc += s1 * pv1;
+  }
+};
+// Mode 6, kernel 2: r = r - alpha helper (CG.hpp:392-393) with helper = A p
+// formed again here (the same per-row sum as kernel 1's, bit for bit, so
+// the same r as update_r's from a stored Ap), and value3 += r.r
+// (CG.hpp:406-407)
+template <typename T> struct EpiUpdR {
+  T *__restrict__ r;
+  T alpha;
+  Dd<T> acc;  // r.r (double-length)
+  T rv, rv1;
+  __device__ __forceinline__ void pre(int i) { rv = r[i]; }
+  __device__ __forceinline__ void pre2c(int i0, int i1, T, T) { pre2(i0, i1); }
+  __device__ __forceinline__ void row(int i, T s) {
+    const T v = rv - alpha * s;
+    r[i] = v;
+    acc += v * v;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    using PV = typename PairOf<T>::V;
+    if (i1 == i0 + 1 && (((uintptr_t)(r + i0)) & (sizeof(PV) - 1)) == 0) {
+      const PV v = *reinterpret_cast<const PV *>(r + i0);
+      rv = v.x;
+      rv1 = v.y;
+    } else {
+      rv = r[i0];
+      rv1 = r[i1];
+    }
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    using PV = typename PairOf<T>::V;
+    const T v0 = rv - alpha * s0, v1 = rv1 - alpha * s1;
+    if (l0 && l1 && (((uintptr_t)(r + i)) & (sizeof(PV) - 1)) == 0) {
+      PV v;
+      v.x = v0;
+      v.y = v1;
+      *reinterpret_cast<PV *>(r + i) = v;
+    } else {
+      if (l0) r[i] = v0;
+      if (l1) r[i + 1] = v1;
+    }
+    if (l0) acc += v0 * v0;
+    if (l1) acc += v1 * v1;
+  }
+};
 template <typename T> struct EpiAccuracy {  // CG.hpp:489-497
   const T *__restrict__ b;
   const T *__restrict__ x;
@@ -2583,6 +2647,57 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean(CsrArgs A, const T *__rest
   EpiDot<T> e{Ap, p, T(0), T(0), T(0)};
   spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
   store_part(ws->pap_part, A.part_off + blockIdx.x - A.wg0, e.acc, sm.red);
+}
+
+// Recomputed-Ap body (mode 6; cgx_abi.cpp enqueue_iter_defer), kernel 1 of
+// 3: the lean walk's A p with only p.Ap kept (no Ap stored: 8 N bytes less
+// written, and kernel 2 reads p instead of Ap, which the walk just pulled
+// through the Infinity Cache)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_lean_dot(CsrArgs A, const T *__restrict__ p,
+                                                          CgScalars<T> *st, int slot,
+                                                          RedWs<T> *ws) {
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiDotOnly<T> e{p, T(0), T(0), T(0)};
+  spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
+  store_part(ws->pap_part, blockIdx.x, e.acc, sm.red);
+}
+
+// Mode 6, kernel 2 of 3: alpha from kernel 1's p.Ap partials (sum_parts, as
+// update_r), the records update_r makes (pAp, alpha, the group's skip
+// mark), then the lean walk forms A p again and updates r in its epilogue;
+// r.r partials for the p update. Every value is mode 3's.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_lean_updr(CsrArgs A, const T *__restrict__ p,
+                                                           T *__restrict__ r, CgScalars<T> *st,
+                                                           int slot, RedWs<T> *ws, int np_pap) {
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T pAp = sum_parts(ws->pap_part, np_pap, sm.red);
+  const T alpha = st->rxr[slot] / pAp;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->pAp[slot] = pAp;
+    st->alpha[slot] = alpha;
+    st->skip[slot] = 0;
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiUpdR<T> e{r, alpha, T(0), T(0), T(0)};
+  spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
+  store_part(ws->rr_part, blockIdx.x, e.acc, sm.red);
 }
 
 // The interior SpMV of a partitioned SELL matrix with the device peer
@@ -4317,6 +4432,25 @@ hipError_t Launch<T>::spmv_dot(const CsrDev &A, const T *p, T *Ap, CgScalars<T> 
   const int v = spmv_variant<T>(A);
   const int spmv_grid_ = cap_resident<T>(grid_rows(A.nrb), v);
   CGX_SPMV_SWITCH(v, k_spmv_dot, a, (const T *)A.val, p, Ap, st, slot, ws);
+}
+template <typename T>
+hipError_t Launch<T>::lean_dot(const CsrDev &A, const T *p, CgScalars<T> *st, int slot,
+                               RedWs<T> *ws, hipStream_t s, int rev) {
+  if (!vl_whole(A)) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  CGX_GGL(k_spmv_lean_dot<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, st, slot, ws);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t Launch<T>::lean_updr(const CsrDev &A, const T *p, T *r, CgScalars<T> *st, int slot,
+                                RedWs<T> *ws, hipStream_t s, int rev) {
+  if (!vl_whole(A)) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  CGX_GGL(k_spmv_lean_updr<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, r, st, slot, ws,
+          A.vl_grid);
+  return hipGetLastError();
 }
 template <typename T>
 hipError_t Launch<T>::spmv_lean_interior(const CsrDev &A, const T *p, T *Ap, CgScalars<T> *st,

@@ -227,6 +227,7 @@ struct cgx_cg {
   bool fused = false;   // two kernels per iteration (x/p update folded into SpMV)
   bool defer = false;   // mode 3: x updated once per 4 bodies from 4 p buffers
   bool fdefer = false;  // mode 4: p update folded into the SpMV, x deferred as mode 3
+  bool recompute = false;  // mode 6 (with defer): Ap formed again in update_r's walk, not stored
   bool coop = false;    // mode 5: persistent body, one launch per chunk (cgx_coop.hip)
   int coop_r = 0;       // its rows per thread
   int coop_stall = -1;  // tests: a launch's body whose p.Ap partial workgroup 0

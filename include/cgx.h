@@ -267,8 +267,11 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * three kernel boundaries; Ap bit-identical, the dots summed in another
  * order (x equal to rounding). $CGX_COOP_R picks its rows per thread,
  * $CGX_COOP_STREAM=1 / 0 always / never the streamed form.
- * Modes 1 and 3 give bit-identical x; so does mode 4 where its SpMV grid is
- * the SpMV's (cgx_csr_fd_grid), else x equal to rounding. */
+ * Mode 6 (round 6; single device, the lean stencil walk): mode 3's body with
+ * no Ap vector — kernel 1 walks A p keeping only p.Ap, kernel 2 walks A p
+ * again and updates r in its epilogue (8 N bytes written and read less).
+ * The dots are double-length sums (round 6), so modes 1, 3, 4 and 6 give
+ * bit-identical x whatever their grids. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
 /* mode 5's launch shape: rows per thread, threads per workgroup (1024),
  * workgroups, and the form: 0 the register form (drained write-through
