@@ -2434,7 +2434,10 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
     return CGX_OK;
   }
   A->dev.lean = false;
-  CGX_REQUIRE(known_variant(variant), CGX_EINVAL, "unknown SpMV variant %d", variant);
+  // (a SELL-family request resolves against the matrix's layout, as the
+  // autotune's own candidates do; the check below refuses one with no kernel)
+  CGX_REQUIRE(known_variant(variant) || (variant & (2048 | 8192)), CGX_EINVAL,
+              "unknown SpMV variant %d", variant);
   CGX_REQUIRE(!(variant & (2048 | 8192)) || A->dev.sl, CGX_EUNSUPPORTED,
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
   CGX_REQUIRE(!(variant & 32768) || A->dev.svc, CGX_EUNSUPPORTED,
@@ -2565,7 +2568,7 @@ int autotune_spmv(cgx_csr *A) {
   // (the pipelined paired loop on the interleaved val / col copy, kIL, is
   // not a candidate: 376 against 373 us at 256^3, 25.3 against 24.9 on the
   // G3 stand-in, 306 against 297 at 4096^2, its stream-only ablation 336
-  // against 324 — profiles/r06f_tune_il_*.log; reachable by request)
+  // against 324 — profiles/r6f_tune_il_*.log; reachable by request)
   if (A->dev.sl) {
     if (!big) cands.push_back(2048);
     cands.push_back(2050);
@@ -3111,6 +3114,10 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
         stream = true;
       }
     }
+    // the whole-matrix lean walk between fd_auto's two bounds (256^3):
+    // mode 6, Ap recomputed by a second walk instead of stored — 5,207-5,214
+    // against 4,920-4,944 it/s in mode 3 (profiles/r6h_mode6_ab.log)
+    if (mode == 3 && !cg->A->dist && vl_whole(cg->A->dev)) mode = 6;
   }
   const bool f = mode == 2, d = mode == 3 || mode == 6, fd = mode == 4, c = mode == 5;
   const bool rc6 = mode == 6;

@@ -40,10 +40,12 @@ def _run(L, q, A, mode, timing, bodies=24):
         L.cgx_cg_destroy(cg)
 
 
-@pytest.mark.parametrize("mode", [1, 3, 4])
+@pytest.mark.parametrize("mode", [1, 3, 4, 6])
 def test_dispatch_recorded_kernel_times(queue, mode):
     L = lib()
     A = cga.Matrix.poisson(queue, 3, 128, 128, 64)
+    if mode == 6:  # (Ap recomputed: the lean walk's mode; forced at this size)
+        check(L.cgx_csr_set_variant(A.schedule(), 33554432))
     x_t, d, dc, e, ec = _run(L, queue, A, mode, True)
     x_g, *_ = _run(L, queue, A, mode, False)
     np.testing.assert_array_equal(x_t, x_g)
