@@ -19,12 +19,17 @@ Poisson CSR (fp64 values, int32 indices, b_i = i + 1, x0 = 0).
   ranks (torch.distributed.run, 127.0.0.1) as a child process before touching
   any GPU; under a launcher, WORLD_SIZE must equal --gpus.
 
-value = the COMPULSORY HBM bytes of one iteration in the formats the kernels
-stream (the SpMV's matrix stream from cgx_csr_stream_bytes, p read and Ap
-written, 24 N for the r update, 34 N average for the deferred x/p update),
-summed over ranks, x iterations/s, in GB/s — a physical figure (<= peak).
-The CSR-priced figure of SURVEY §8(d) (B_alg = 12 nnz + 4 (N+1) + 80 N) is
-reported beside it as `csr_equivalent_GBs`.
+value = CG iterations (bodies) per second of the whole job, the metric's first
+quantity (round 6: it was the GB/s figure below, which a body that moves
+fewer bytes — mode 6, Ap formed again instead of stored — lowers while it
+raises iterations/s). achieved_GBs = the COMPULSORY HBM bytes of one
+iteration in the formats the kernels stream (the SpMV's matrix stream from
+cgx_csr_stream_bytes, p read and Ap written — mode 6: p read twice, no Ap —,
+24 N for the r update, 34 N average for the deferred x/p update), summed
+over ranks, x iterations/s, in GB/s: a physical figure (<= peak), and
+iteration_frac = achieved_GBs / (peak x N). The CSR-priced figure of SURVEY
+§8(d) (B_alg = 12 nnz + 4 (N+1) + 80 N) is reported beside it as
+`csr_equivalent_GBs`.
 
 The timed region replays hipGraphs of the iteration (no per-kernel events).
 Right after it, `--profile-steps` more iterations run with HIP events around
@@ -615,31 +620,43 @@ def run(args) -> None:
         roof = coop_roofline(L, cg, avg, calls, args.profile_steps, iter_local)
     elif calls[1] > 0:
         kb = spmv_fmt_local + (32 * n_local if fused else 0)
-        ach = kb / (avg[1] * 1e-3) / 1e9
+        # mode 6: the walk runs in kernels 1 (p.Ap only) and 2 (r updated in
+        # its epilogue); kernel 2 is the larger, and the roofline's
+        kid = 2 if mode_eff == 6 else 1
+        if mode_eff == 6:
+            kb = sbytes.value + 24 * n_local
+        ach = kb / (avg[kid] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
             (16 * n_local if mode_eff == 4 else 0)
         kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" + sfx if lean_on else "k_spmv_fd",
-                 6: "k_spmv_lean_dot"}.get(mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
+                 6: "k_spmv_lean_updr"}.get(mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname,
                 "bytes_per_launch": kb,
-                "bytes_basis": "compulsory bytes of the kernel's own format: matrix stream "
-                               "(cgx_csr_stream_bytes) + p read + Ap written" +
-                               (" + r read + p_k written" if mode_eff == 4 else ""),
-                "avg_us": round(avg[1] * 1e3, 2), "launches_timed": int(calls[1]),
+                "bytes_basis": ("compulsory bytes of the kernel's own format: matrix stream "
+                                "(cgx_csr_stream_bytes) + p read + r read + r written (A p "
+                                "formed again, no Ap vector)" if mode_eff == 6 else
+                                "compulsory bytes of the kernel's own format: matrix stream "
+                                "(cgx_csr_stream_bytes) + p read + Ap written" +
+                                (" + r read + p_k written" if mode_eff == 4 else "")),
+                "avg_us": round(avg[kid] * 1e3, 2), "launches_timed": int(calls[kid]),
                 "avg_us_basis": "HIP events recorded by each launch's dispatch "
                                 "(hipExtLaunchKernel start/stop) on the solver stream",
-                "avg_us_with_dispatch": round(avg_d[1] * 1e3, 2),
+                "avg_us_with_dispatch": round(avg_d[kid] * 1e3, 2),
                 "csr_equivalent_bytes_per_launch": cb,
-                "csr_equivalent_GBs": round(cb / (avg[1] * 1e-3) / 1e9, 1),
+                "csr_equivalent_GBs": round(cb / (avg[kid] * 1e-3) / 1e9, 1),
                 "other_kernels_avg_us": {"k_update_r": round(avg[2] * 1e3, 2)}}
         if mode_eff == 4:  # every fourth k_update_r also applies the group's x updates
             roof["other_kernels_avg_us"] = {"k_update_r (+ x flush in 1 of 4)":
                                             round(avg[2] * 1e3, 2)}
         elif mode_eff == 6:
-            roof["other_kernels_avg_us"] = {"k_spmv_lean_updr": round(avg[2] * 1e3, 2),
+            kb1 = sbytes.value + 8 * n_local  # the walk's p.Ap: matrix stream + p read
+            roof["other_kernels_avg_us"] = {"k_spmv_lean_dot": round(avg[1] * 1e3, 2),
                                             "k_update_p": round(avg[3] * 1e3, 2)}
+            roof["k_spmv_lean_dot"] = {"bytes_per_launch": kb1, "avg_us": round(avg[1] * 1e3, 2),
+                                       "frac": round(kb1 / (avg[1] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                     4)}
         elif not fused:
             roof["other_kernels_avg_us"]["k_update_p"] = round(avg[3] * 1e3, 2)
         if world == 1 and not args.no_traffic:
@@ -677,8 +694,8 @@ def run(args) -> None:
         workload = wl.description
         line = {
             "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GB/s",
+            "value": round(its, 2),
+            "unit": "it/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -691,8 +708,10 @@ def run(args) -> None:
             "data": ("synthetic (Dirichlet Poisson CSR generated in HBM, b_i = i + 1, x0 = 0)"
                      if args.workload in workloads.POISSON else
                      "synthetic (see config.workload; b_i = i + 1, x0 = 0)"),
-            "value_basis": "compulsory HBM bytes per iteration in the streamed formats "
-                           "(all ranks) x iterations/s",
+            "value_basis": "CG iterations (bodies) per second of the whole job; "
+                           "achieved_GBs: compulsory HBM bytes per iteration in the streamed "
+                           "formats (all ranks) x iterations/s",
+            "achieved_GBs": round(value, 2),
             "bytes_per_iteration": iter_global,
             "iteration_frac": round(value / (HBM_PEAK_GBS * world), 4),
             "csr_equivalent_GBs": round(csr_eq, 2),
@@ -957,6 +976,9 @@ def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):
     out = {}
     orig = C.c_int(0)
     check(L.cgx_csr_variant(A, C.byref(orig)))
+    # (mode 6 recomputes Ap with the lean walk; the general formats run its
+    # stored-Ap body, mode 3)
+    mode_eff = 3 if mode_eff == 6 else mode_eff
     for name, req in (("sellp_plain", 8194), ("csr_stream", 15)):
         try:
             check(L.cgx_csr_set_variant(A, req))

@@ -2436,8 +2436,11 @@ extern "C" int cgx_csr_set_variant(cgx_csr *A, int variant) {
   A->dev.lean = false;
   // (a SELL-family request resolves against the matrix's layout, as the
   // autotune's own candidates do; the check below refuses one with no kernel)
-  CGX_REQUIRE(known_variant(variant) || (variant & (2048 | 8192)), CGX_EINVAL,
-              "unknown SpMV variant %d", variant);
+  constexpr int kSellBits = 2 | 16 | 2048 | 4096 | 8192 | 16384 | 32768 | 262144 | 524288 |
+                            1048576 | 2097152 | kVT;
+  CGX_REQUIRE(known_variant(variant) ||
+                  ((variant & (2048 | 8192)) && (variant & ~kSellBits) == 0),
+              CGX_EINVAL, "unknown SpMV variant %d", variant);
   CGX_REQUIRE(!(variant & (2048 | 8192)) || A->dev.sl, CGX_EUNSUPPORTED,
               "variant %d needs the SELL-64 copy, which this matrix does not have", variant);
   CGX_REQUIRE(!(variant & 32768) || A->dev.svc, CGX_EUNSUPPORTED,

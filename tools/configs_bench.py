@@ -60,7 +60,7 @@ def main():
         kern = (f"{r.get('kernel')}{r['template']} (whole body)" if r.get("template")
                 else f"{r.get('kernel')}<{ln['config']['spmv_variant']}>")
         us = r.get("us_per_body") or r.get("avg_us")
-        print(f"| {name} | {ln['iterations_per_s']:,} | {ln['value']:,} | {ln['iteration_frac']} | "
+        print(f"| {name} | {ln['iterations_per_s']:,} | {ln['achieved_GBs']:,} | {ln['iteration_frac']} | "
               f"{kern} | {us} | "
               f"{r.get('frac')} | {r.get('traffic_ratio_to_compulsory')} | "
               f"{ln['csr_equivalent_GBs']:,} |", flush=True)

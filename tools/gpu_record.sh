@@ -3,7 +3,8 @@
 # driver's bench command, rocprofv3 --kernel-trace --stats of that same
 # command, FETCH_SIZE / WRITE_SIZE PMC passes (separate runs), the per-config
 # lines. Stops at the first failing GPU step. Outputs in gpurun_out/$TAG.
-#   tools/gpu_record.sh TAG [quick]     (quick: skip pytest)
+#   tools/gpu_record.sh TAG [quick|full] [noconfigs]   (quick: skip pytest; noconfigs:
+#   stop after the PMC passes)
 set -o pipefail
 TAG=${1:-rec}
 OUT=gpurun_out/$TAG
@@ -24,6 +25,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 -s KILL 300 rocprofv3 --pmc $C -d $OUT/pmc_$C -o run --output-format csv -- python3 bench.py --no-cpu --no-general --steps 10 --warmup 2 --profile-steps 0 > $OUT/pmc_$C.log 2>&1 || { echo "PMC $C FAIL"; tail -20 $OUT/pmc_$C.log; exit 1; }
   echo "pmc $C ok"
 done
+[ "$3" = "noconfigs" ] && exit 0
 timeout -k 10 600 python tools/configs_bench.py > $OUT/configs.log 2>&1 || { echo CONFIGS_FAIL; tail -20 $OUT/configs.log; exit 1; }
 cut -c1-240 $OUT/configs.log
 timeout -k 10 400 bash tools/gpu_slab.sh $TAG/slab > $OUT/slab_all.log 2>&1 || { echo SLAB_FAIL; tail -20 $OUT/slab_all.log; exit 1; }
