@@ -2667,6 +2667,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean_dot(CsrArgs A, const T *__
     vt = sm.vt;
   }
   EpiDotOnly<T> e{p, T(0), T(0), T(0)};
+  // (the walk with the next slice's gathers issued before the current
+  // slice's sums ran 54.4 against 39-40 us here: profiles/r6m_lean_dot_prefetch_ab.log)
   spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
   store_part(ws->pap_part, blockIdx.x, e.acc, sm.red);
 }
