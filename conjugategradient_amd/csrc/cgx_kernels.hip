@@ -191,11 +191,13 @@ __device__ __forceinline__ void lds_barrier() {
 // reduces over the workgroup through LDS with LDS-only barriers, so loads
 // issued after parts_load stay in flight (vmcnt waits in issue order).
 constexpr int kPartsPerThread = 2 * kMaxGrid / kBlock;  // split SpMV: 2 launches
-template <typename T>
-__device__ __forceinline__ void parts_load(const T *__restrict__ part, int np,
-                                           Dd<T> (&pl)[kPartsPerThread]) {
+// (KP: the loads per thread, a launch's bound on ceil(np / kBlock); the
+// vector kernels are instantiated for 4, 8 and 16 so a launch after a
+// 1,024-workgroup SpMV does not issue 16)
+template <typename T, int KP>
+__device__ __forceinline__ void parts_load(const T *__restrict__ part, int np, Dd<T> (&pl)[KP]) {
 #pragma unroll
-  for (int k = 0; k < kPartsPerThread; ++k)  // unconditional (np >= 1): exact vmcnt waits
+  for (int k = 0; k < KP; ++k)  // unconditional (np >= 1): exact vmcnt waits
     pl[k] = load_part(part, min((int)threadIdx.x + k * kBlock, np - 1));
 }
 // parts_load for a kernel with no stream loads behind it: only the np
@@ -210,13 +212,12 @@ __device__ __forceinline__ void parts_load_np(const T *__restrict__ part, int np
     pl[k] = i < np ? load_part(part, i) : Dd<T>(T(0));
   }
 }
-template <typename T>
-__device__ __forceinline__ Dd<T> parts_sum_dd(const Dd<T> (&pl)[kPartsPerThread], int np,
-                                              T *lds) {
+template <typename T, int KP>
+__device__ __forceinline__ Dd<T> parts_sum_dd(const Dd<T> (&pl)[KP], int np, T *lds) {
   __shared__ T bc[2];
   Dd<T> v(T(0));
 #pragma unroll
-  for (int k = 0; k < kPartsPerThread; ++k)
+  for (int k = 0; k < KP; ++k)
     if ((int)threadIdx.x + k * kBlock < np) v += pl[k];  // sum_parts order
   v = wave_sum_dd(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -235,8 +236,8 @@ __device__ __forceinline__ Dd<T> parts_sum_dd(const Dd<T> (&pl)[kPartsPerThread]
   lds_barrier();
   return Dd<T>(bc[0], bc[1]);
 }
-template <typename T>
-__device__ __forceinline__ T parts_sum(const Dd<T> (&pl)[kPartsPerThread], int np, T *lds) {
+template <typename T, int KP>
+__device__ __forceinline__ T parts_sum(const Dd<T> (&pl)[KP], int np, T *lds) {
   return parts_sum_dd(pl, np, lds).value();
 }
 
@@ -3145,7 +3146,7 @@ __device__ __forceinline__ void flush_group_range(int64_t n, T *__restrict__ x,
 }
 
 
-template <typename T, bool FUSED, bool PEER, bool SNT, bool GF = false>
+template <typename T, bool FUSED, bool PEER, bool SNT, bool GF = false, int KP = kPartsPerThread>
 // rin == r: in place (modes 1, 2); else r ping-pongs between two buffers.
 // GF (mode 4, slot 3): after r, the group's deferred x updates (xf), also
 // when the body itself is inactive (the group's earlier bodies that ran).
@@ -3177,7 +3178,7 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   // make its wait drain the prefetch too
   const T rxr = cst->rxr[slot];
   const T pAp_st = cst->pAp[slot];
-  Dd<T> pl[kPartsPerThread];
+  Dd<T> pl[KP];
   const bool from_parts = !FUSED && np_pap > 0;
   if (from_parts) parts_load(ws->pap_part, np_pap, pl);
   V rv[kUR], av[kUR];
@@ -3312,32 +3313,33 @@ __device__ __forceinline__ void update_r_body(int64_t n, const T *rin, T *r,
   }
 }
 
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, int KP = kPartsPerThread>
 __global__ __launch_bounds__(kBlock) void k_update_r(int64_t n, const T *rin, T *r,
                                                      const T *__restrict__ Ap,
                                                      CgScalars<T> *st, int slot,
                                                      RedWs<T> *ws, int np_pap, int rev,
                                                      int rule) {
   if (stream_nt<T>(n))
-    update_r_body<T, FUSED, false, true>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule, nullptr);
+    update_r_body<T, FUSED, false, true, false, KP>(n, rin, r, Ap, st, slot, ws, np_pap, rev,
+                                                    rule, nullptr);
   else
-    update_r_body<T, FUSED, false, false>(n, rin, r, Ap, st, slot, ws, np_pap, rev, rule,
-                                          nullptr);
+    update_r_body<T, FUSED, false, false, false, KP>(n, rin, r, Ap, st, slot, ws, np_pap, rev,
+                                                     rule, nullptr);
 }
 // Mode 4, slot 3: update_r with the stop rule and the group's x flush in one
 // launch (k_flush_group's values, bit for bit)
-template <typename T>
+template <typename T, int KP = kPartsPerThread>
 __global__ __launch_bounds__(kBlock) void k_update_r_flush(int64_t n, T *r,
                                                            const T *__restrict__ Ap,
                                                            CgScalars<T> *st, int slot,
                                                            RedWs<T> *ws, int np_pap, int rev,
                                                            XFlush<T> xf) {
   if (stream_nt<T>(n))
-    update_r_body<T, false, false, true, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1, nullptr,
-                                               &xf);
+    update_r_body<T, false, false, true, true, KP>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1,
+                                                   nullptr, &xf);
   else
-    update_r_body<T, false, false, false, true>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1,
-                                                nullptr, &xf);
+    update_r_body<T, false, false, false, true, KP>(n, r, r, Ap, st, slot, ws, np_pap, rev, 1,
+                                                    nullptr, &xf);
 }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_update_r_peer(int64_t n, T *r,
@@ -4531,8 +4533,16 @@ hipError_t Launch<T>::update_r(int64_t n, T *r, const T *Ap, CgScalars<T> *st, i
                        n, rin, r,
                        Ap, st, slot, ws, 0, 0, 0);
   } else {
-    CGX_GGL((k_update_r<T, false>), dim3(grid_elems(n, kGridUpdateR)), dim3(kBlock), 0,
-                       s, n, rin, r, Ap, st, slot, ws, np_pap, rev, rule);
+    const int g = grid_elems(n, kGridUpdateR);
+    if (np_pap <= 4 * kBlock)
+      CGX_GGL((k_update_r<T, false, 4>), dim3(g), dim3(kBlock), 0, s, n, rin, r, Ap, st, slot,
+              ws, np_pap, rev, rule);
+    else if (np_pap <= 8 * kBlock)
+      CGX_GGL((k_update_r<T, false, 8>), dim3(g), dim3(kBlock), 0, s, n, rin, r, Ap, st, slot,
+              ws, np_pap, rev, rule);
+    else
+      CGX_GGL((k_update_r<T, false>), dim3(g), dim3(kBlock), 0, s, n, rin, r, Ap, st, slot, ws,
+              np_pap, rev, rule);
   }
   return hipGetLastError();
 }
@@ -4752,6 +4762,12 @@ hipError_t Launch<T>::update_r_flush(int64_t n, T *r, const T *Ap, CgScalars<T> 
                                      RedWs<T> *ws, int np_pap, int rev, T *x, T *const P[4],
                                      hipStream_t s) {
   const XFlush<T> xf{x, {P[0], P[1], P[2], P[3]}};
+  if (np_pap <= 4 * kBlock)
+    CGX_LAUNCH((k_update_r_flush<T, 4>), grid_elems(n, kGridUpdateR), n, r, Ap, st, slot, ws,
+               np_pap, rev, xf);
+  if (np_pap <= 8 * kBlock)
+    CGX_LAUNCH((k_update_r_flush<T, 8>), grid_elems(n, kGridUpdateR), n, r, Ap, st, slot, ws,
+               np_pap, rev, xf);
   CGX_LAUNCH(k_update_r_flush<T>, grid_elems(n, kGridUpdateR), n, r, Ap, st, slot, ws, np_pap,
              rev, xf);
 }
