@@ -89,9 +89,45 @@ def allreduce(v: float) -> float:
     return float(t.item())
 
 
-def solve(plan, val_local, b_local, tol, oracle, n_global):
+def _two_sum_into(s, x):
+    """s = [hi, lo] += x (TwoSum, cgx_dd.h Dd::operator+=)."""
+    hi = s[0]
+    t = hi + x
+    z = t - hi
+    s[1] += (hi - (t - z)) + (x - z)
+    s[0] = t
+
+
+def dd_dot(a, b):
+    """This rank's double-length sum of the rounded products a_i b_i."""
+    s = [0.0, 0.0]
+    for x in (np.asarray(a) * np.asarray(b)).tolist():
+        _two_sum_into(s, x)
+    return s
+
+
+def dd_allreduce(pair) -> float:
+    """The peer transport's world sum (cgx_peer_dev.h world_sum): every
+    rank's pair, combined in rank order as pairs, rounded once."""
+    pairs = [None] * dist.get_world_size()
+    dist.all_gather_object(pairs, (float(pair[0]), float(pair[1])))
+    s = [pairs[0][0], pairs[0][1]]
+    for hi, lo in pairs[1:]:
+        _two_sum_into(s, hi)
+        s[1] += lo
+    return s[0] + s[1]
+
+
+def solve(plan, val_local, b_local, tol, oracle, n_global, dots="plain"):
     """libcgx's iteration (k_spmv_dot / k_update_r / k_update_xp) with the
-    reference's stop rule; returns (x_local, bodies)."""
+    reference's stop rule; returns (x_local, bodies). dots="dd": every dot a
+    double-length sum per rank and a pair world sum (round 6's engine)."""
+    if dots == "dd":
+        def gdot(u, v):
+            return dd_allreduce(dd_dot(u, v))
+    else:
+        def gdot(u, v):
+            return allreduce(oracle.dot_acc(u, v, 0.0))
     nl = plan["n_local"]
     ng = len(plan["ghosts"])
     rp, cl = plan["rowptr"], plan["col"]
@@ -101,16 +137,16 @@ def solve(plan, val_local, b_local, tol, oracle, n_global):
     r = b_local - oracle.spmv(rp, cl, val_local, xe)
     p = np.zeros(nl + ng)
     p[:nl] = r
-    rxr = allreduce(oracle.dot_acc(r, r, 0.0))
+    rxr = gdot(r, r)
     bodies = 0
     cap = n_global + 1
     while True:
         halo(plan, p)
         Ap = oracle.spmv(rp, cl, val_local, p)
-        pAp = allreduce(oracle.dot_acc(Ap, p[:nl], 0.0))
+        pAp = gdot(Ap, p[:nl])
         alpha = rxr / pAp
         r = oracle.sambx(r, Ap, alpha)
-        rr = allreduce(oracle.dot_acc(r, r, 0.0))
+        rr = gdot(r, r)
         beta = rr / rxr
         x = oracle.sapbx(x, p[:nl], alpha)
         p[:nl] = oracle.sapbx(r, p[:nl], beta)
