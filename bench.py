@@ -81,8 +81,10 @@ def update_bytes_per_iter(n: int, mode: int) -> int:
     (24 n) in three bodies of four and in the fourth also applies
     x += a0 p0 + .. + a3 p3 (reads x and the three other p buffers, writes x:
     +40 n), 34 n on average."""
-    if mode == 4:  # the p update is folded into the SpMV (spmv_bytes_per_iter);
-        return 24 * n + 12 * n  # the slot-3 x flush: x r/w + 4 p reads, once per 4 bodies
+    if mode in (4, 7):  # the p update is folded into the SpMV (spmv_bytes_per_iter);
+        # the slot-3 x flush: x r/w + 4 p reads, once per 4 bodies (mode 7:
+        # kernel 2 reads p_k where update_r reads Ap, plus its matrix stream)
+        return 24 * n + 12 * n
     # mode 6: kernel 2 reads p (A p formed again) where update_r reads Ap: the
     # same 24 n, plus its matrix stream (added by the caller)
     xp = 40 * n if mode in (1, 5) else 34 * n  # mode 5: priced as mode 1
@@ -93,7 +95,8 @@ def spmv_bytes_per_iter(stream_bytes: int, n: int, mode: int) -> int:
     """The SpMV launch: its matrix stream (cgx_csr_stream_bytes) + p read + Ap
     written (16 n); mode 4's k_spmv_fd reads r and p_{k-1} and writes p_k and
     Ap (32 n)."""
-    return stream_bytes + (32 * n if mode == 4 else 8 * n if mode == 6 else 16 * n)
+    return stream_bytes + (32 * n if mode == 4 else 8 * n if mode == 6 else
+                           24 * n if mode == 7 else 16 * n)
 
 
 def warmup_run(args) -> int:
@@ -134,7 +137,7 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=100,
                     help="iterations timed per kernel with HIP events after the timed region "
                          "(0: skip the roofline pass)")
-    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4, 5, 6], default=0,
+    ap.add_argument("--mode", type=int, choices=[0, 1, 2, 3, 4, 5, 6, 7], default=0,
                     help="iteration structure (cgx_cg_set_mode): 0 auto, 1 three kernels, "
                          "2 fused (single GPU), 3 three kernels with the x update deferred, "
                          "4 two kernels (p update folded into the SpMV), x deferred")
@@ -606,7 +609,7 @@ def run(args) -> None:
     # compulsory bytes of one iteration in the streamed formats, all ranks
     spmv_fmt_local = spmv_bytes_per_iter(sbytes.value, n_local, mode_eff)
     iter_local = spmv_fmt_local + update_bytes_per_iter(n_local, mode_eff)
-    if mode_eff == 6:  # kernel 2's walk streams the matrix's format again
+    if mode_eff in (6, 7):  # kernel 2's walk streams the matrix's format again
         iter_local += sbytes.value
     if fused:
         iter_local = sbytes.value + 48 * n_local + 24 * n_local
@@ -646,18 +649,27 @@ def run(args) -> None:
         kid = 2 if mode_eff == 6 else 1
         if mode_eff == 6:
             kb = sbytes.value + 24 * n_local
+        if mode_eff == 7:  # two walks of 24 N each: the longer one
+            kid = 2 if avg[2] >= avg[1] else 1
+            kb = sbytes.value + 24 * n_local
         ach = kb / (avg[kid] * 1e-3) / 1e9
         cb = csr_spmv_bytes(n_local, nnz_local) + (32 * n_local if fused else 0) + \
             (16 * n_local if mode_eff == 4 else 0)
         kname = {2: "k_spmv_fused", 4: "k_spmv_fd_lean" + sfx if lean_on else "k_spmv_fd",
-                 6: "k_spmv_lean_updr"}.get(mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
+                 6: "k_spmv_lean_updr",
+                 7: "k_spmv_lean_updr_rule" if kid == 2 else "k_spmv_fd_dot_tile"
+                 }.get(mode_eff, "k_spmv_lean" if lean_on else "k_spmv_dot")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname,
                 "bytes_per_launch": kb,
                 "bytes_basis": ("compulsory bytes of the kernel's own format: matrix stream "
-                                "(cgx_csr_stream_bytes) + p read + r read + r written (A p "
-                                "formed again, no Ap vector)" if mode_eff == 6 else
+                                "(cgx_csr_stream_bytes) + p_k read + r read + r written (A "
+                                "p_k formed again, no Ap vector)" if kname.startswith(
+                                    "k_spmv_lean_updr") else
+                                "compulsory bytes of the kernel's own format: matrix stream "
+                                "(cgx_csr_stream_bytes) + r read + p_{k-1} read + p_k written "
+                                "(no Ap vector)" if kname == "k_spmv_fd_dot_tile" else
                                 "compulsory bytes of the kernel's own format: matrix stream "
                                 "(cgx_csr_stream_bytes) + p read + Ap written" +
                                 (" + r read + p_k written" if mode_eff == 4 else "")),
@@ -671,6 +683,13 @@ def run(args) -> None:
         if mode_eff == 4:  # every fourth k_update_r also applies the group's x updates
             roof["other_kernels_avg_us"] = {"k_update_r (+ x flush in 1 of 4)":
                                             round(avg[2] * 1e3, 2)}
+        elif mode_eff == 7:
+            other = 1 if kid == 2 else 2
+            roof["other_kernels_avg_us"] = {
+                ("k_spmv_fd_dot_tile" if other == 1 else "k_spmv_lean_updr_rule"):
+                    round(avg[other] * 1e3, 2),
+                "k_flush_group (slot 3 only)": round(avg[3] * 1e3, 2)}
+            roof["other_walk_frac"] = round(kb / (avg[other] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         elif mode_eff == 6:
             kb1 = sbytes.value + 8 * n_local  # the walk's p.Ap: matrix stream + p read
             roof["other_kernels_avg_us"] = {"k_spmv_lean_dot": round(avg[1] * 1e3, 2),
@@ -689,7 +708,8 @@ def run(args) -> None:
             roof["traffic_by_kernel"] = t.get("by_kernel")
             roof["traffic_method"] = t.get("method")
             key = ("k_spmv_fd_lean_t<double, true, true>" if kname == "k_spmv_fd_lean_t"
-                   else f"{kname}<double>" if kname.startswith(("k_spmv_lean", "k_spmv_fd_lean"))
+                   else f"{kname}<double>" if kname.startswith(("k_spmv_lean", "k_spmv_fd_lean",
+                                                                 "k_spmv_fd_dot"))
                    else f"{kname}<double, {int(variant.value & ~KVL)}>")
             if t.get("by_kernel") and key in t["by_kernel"]:
                 roof["traffic"] = t["by_kernel"][key]
@@ -761,7 +781,12 @@ def run(args) -> None:
                                         "grid-wide exchanges per body)",
                                      6: "3 kernels, Ap recomputed (the walk's p.Ap; the walk "
                                         "again with r -= alpha A p; the p update), x update "
-                                        "deferred over 4 bodies"}[mode_eff] +
+                                        "deferred over 4 bodies",
+                                     7: "2 kernels, p update in the first walk and Ap "
+                                        "recomputed (the tile walk forming p_k with p.Ap; the "
+                                        "walk again with r -= alpha A p_k and the stop rule), "
+                                        "x update deferred over 4 bodies (+ a flush launch in "
+                                        "slot 3)"}[mode_eff] +
                                     (" (auto)" if args.mode == 0 else ""),
                        "setup": setup,
                        "spmv_variant": int(variant.value),
@@ -1000,7 +1025,7 @@ def general_formats(L, q, A, b, x, n, nnz, mode_eff, args, steps=100, prof=50):
     check(L.cgx_csr_variant(A, C.byref(orig)))
     # (mode 6 recomputes Ap with the lean walk; the general formats run its
     # stored-Ap body, mode 3)
-    mode_eff = 3 if mode_eff == 6 else mode_eff
+    mode_eff = 3 if mode_eff in (6, 7) else mode_eff
     for name, req in (("sellp_plain", 8194), ("csr_stream", 15)):
         try:
             check(L.cgx_csr_set_variant(A, req))

@@ -449,6 +449,24 @@ template <typename T> int enqueue_iter_fdefer(cgx_cg *cg, int slot) {
                                            slot == 3 ? P : nullptr, s, PD);
     });
   }
+  if (cg->recompute) {
+    // mode 7: kernel 1 forms p_k into P[slot] with p.Ap only (the tile walk,
+    // no Ap vector), kernel 2 forms A p_k again from it and updates r with
+    // the stop rule; slot 3 applies the group's x updates after it
+    // (k_flush_group). 60 N bytes per body against mode 6's 66 N.
+    if ((rc = timed(cg, 1, s, [&] {
+           return Launch<T>::fd_dot_tile(A->dev, r, P[(slot + 3) & 3], P[slot], st, slot, ws,
+                                         A->dev.vl_grid, s, par);
+         })))
+      return rc;
+    if ((rc = timed(cg, 2, s, [&] {
+           return Launch<T>::lean_updr_rule(A->dev, P[slot], r, st, slot, ws, s, rpar);
+         })))
+      return rc;
+    if (slot == 3)
+      return timed(cg, 3, s, [&] { return Launch<T>::flush_group(cg->n, x, P, st, s, par); });
+    return CGX_OK;
+  }
   const int npp = Launch<T>::fd_parts(A->dev);
   if ((rc = timed(cg, 1, s, [&] {
          return Launch<T>::spmv_fd(A->dev, r, P[(slot + 3) & 3], P[slot], Ap, st, slot, ws, npr,
@@ -529,8 +547,10 @@ int flush_pending_x(cgx_cg *cg) {
     // bodies of an unfinished group (a finished one was applied by its slot-3
     // flush), then the final r.r record when the run ended on an active body
     hipStream_t s = cg->ctx->stream;
-    const int npr = cg->dtype == CGX_F32 ? Launch<float>::update_parts(cg->n)
-                                         : Launch<double>::update_parts(cg->n);
+    // (mode 7: kernel 2 is the lean walk, one r.r partial per workgroup)
+    const int npr = cg->recompute ? cg->A->dev.vl_grid
+                    : cg->dtype == CGX_F32 ? Launch<float>::update_parts(cg->n)
+                                           : Launch<double>::update_parts(cg->n);
     if (cg->dtype == CGX_F32) {
       float *P[4] = {(float *)cg->p, (float *)cg->pk[0], (float *)cg->pk[1], (float *)cg->pk[2]};
       if (cg->slot != 0)
@@ -2961,7 +2981,7 @@ extern "C" int cgx_cg_create(cgx_ctx *ctx, cgx_csr *A, cgx_cg **out) {
   // (mode 3: +4-8% over mode 1 at 256^3) or, where it pays,
   // two (mode 4, fd_auto); plain three kernels when the three extra p buffers
   // do not fit
-  if (cgx_cg_set_mode(cg, 0) != CGX_OK) cg->defer = cg->fdefer = false;
+  if (cgx_cg_set_mode(cg, 0) != CGX_OK) cg->defer = cg->fdefer = cg->recompute = false;
   return CGX_OK;
 }
 
@@ -3056,11 +3076,16 @@ static bool coop_auto(const cgx_cg *cg) {
 
 extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
   CGX_REQUIRE(cg, CGX_EINVAL, "cg is NULL");
-  CGX_REQUIRE(mode >= 0 && mode <= 6, CGX_EINVAL,
+  CGX_REQUIRE(mode >= 0 && mode <= 7, CGX_EINVAL,
               "mode %d: 0 auto, 1 three kernels, 2 fused, 3 three kernels with deferred x, "
-              "4 fused with deferred x, 5 persistent body, 6 recomputed Ap", mode);
+              "4 fused with deferred x, 5 persistent body, 6 recomputed Ap, 7 fused with "
+              "recomputed Ap", mode);
   CGX_REQUIRE(mode != 6 || (!cg->A->dist && vl_whole(cg->A->dev)), CGX_EUNSUPPORTED,
               "mode 6 (recomputed Ap) needs the lean stencil walk on a single device");
+  CGX_REQUIRE(mode != 7 || (!cg->A->dist && cg->dtype == CGX_F64 && lean_tile_ok(cg->A->dev)),
+              CGX_EUNSUPPORTED,
+              "mode 7 (fused, recomputed Ap) needs f64 and the tile form of the lean stencil walk "
+              "(a 3-D stencil layout, one plane per step) on a single device");
   int coop_r = 0;
   if (!cg->begun) {  // mode 5's form and test hook
     cg->coop_stall = -1;
@@ -3122,8 +3147,8 @@ extern "C" int cgx_cg_set_mode(cgx_cg *cg, int mode) {
     // against 4,920-4,944 it/s in mode 3 (profiles/r6h_mode6_ab.log)
     if (mode == 3 && !cg->A->dist && vl_whole(cg->A->dev)) mode = 6;
   }
-  const bool f = mode == 2, d = mode == 3 || mode == 6, fd = mode == 4, c = mode == 5;
-  const bool rc6 = mode == 6;
+  const bool f = mode == 2, d = mode == 3 || mode == 6, fd = mode == 4 || mode == 7, c = mode == 5;
+  const bool rc6 = mode == 6 || mode == 7;
   if (f != cg->fused || d != cg->defer || fd != cg->fdefer || c != cg->coop ||
       rc6 != cg->recompute) {
     CGX_REQUIRE(!cg->begun, CGX_ESTATE, "set the mode before cgx_cg_begin");
@@ -3187,7 +3212,12 @@ extern "C" int cgx_csr_fd_grid(cgx_csr *A, int *fd_grid, int *spmv_grid) {
 
 extern "C" int cgx_cg_get_mode(cgx_cg *cg, int *mode) {
   CGX_REQUIRE(cg && mode, CGX_EINVAL, "NULL argument");
-  *mode = cg->coop ? 5 : cg->fdefer ? 4 : cg->recompute ? 6 : cg->defer ? 3 : cg->fused ? 2 : 1;
+  *mode = cg->coop       ? 5
+          : cg->fdefer   ? (cg->recompute ? 7 : 4)
+          : cg->recompute ? 6
+          : cg->defer     ? 3
+          : cg->fused     ? 2
+                          : 1;
   return CGX_OK;
 }
 

@@ -246,6 +246,11 @@ __host__ __device__ inline bool vl_active(const CsrDev &A) {
 __host__ __device__ inline bool vl_whole(const CsrDev &A) {
   return vl_active(A) && !A.vl_split && !A.sell_partial;
 }
+// the tile form of the lean walk (cgx_kernels.hip spmv_lean_tile) applies,
+// and the partial count of its launches (modes 6 and 7's kernel 1)
+bool lean_tile_ok(const CsrDev &A);
+int lean_dot_parts(const CsrDev &A);
+int fd_dot_parts(const CsrDev &A);  // mode 7's kernel 1 (lean_tile_ok)
 
 // Kernel-execution timing (cgx_abi.cpp timed(), kernel timing on): the next
 // launch takes these start / stop events, recorded by its dispatch itself
@@ -302,6 +307,13 @@ template <typename T> struct Launch {
   // walk again with r -= alpha (A p) in its epilogue, r.r partials [0, vl_grid)
   static hipError_t lean_dot(const CsrDev &A, const T *p, CgScalars<T> *st, int slot,
                              RedWs<T> *ws, hipStream_t s, int rev);
+  // mode 7 (lean_tile_ok): the fused walk forming p_k with p.Ap only, then
+  // the recomputing r update with the stop rule
+  static hipError_t fd_dot_tile(const CsrDev &A, const T *r, const T *pold, T *pc,
+                                CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
+                                hipStream_t s, int rev);
+  static hipError_t lean_updr_rule(const CsrDev &A, const T *p, T *r, CgScalars<T> *st, int slot,
+                                   RedWs<T> *ws, hipStream_t s, int rev);
   static hipError_t lean_updr(const CsrDev &A, const T *p, T *r, CgScalars<T> *st, int slot,
                               RedWs<T> *ws, hipStream_t s, int rev);
   // a partitioned matrix's interior slices by the lean walk (A.vl_split), the

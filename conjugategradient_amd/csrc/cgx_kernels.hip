@@ -548,6 +548,13 @@ template <typename T> struct GatherX {
   __device__ __forceinline__ T at_s(int i) const {
     return ((const __attribute__((address_space(4))) T *)x)[i];
   }
+  // the tile walk's loads and their values (GatherP forms p_k from its pair)
+  using Raw = typename PairU<T>::V;
+  using Raw1 = T;
+  __device__ __forceinline__ Raw raw_b(unsigned b) const { return pair_b(b); }
+  __device__ __forceinline__ Raw form(const Raw &w) const { return w; }
+  __device__ __forceinline__ Raw1 raw1(int i) const { return x[i]; }
+  __device__ __forceinline__ T form1(const Raw1 &w) const { return w; }
 };
 // The boundary slices of a partitioned matrix with the peer transport's wait
 // folded in (k_spmv_dot_bnd): x below n is this rank's p, from n on the
@@ -627,6 +634,11 @@ template <typename T, bool NTP = false> struct GatherP {
     o.y = w.a.y + beta * w.q.y;
     return o;
   }
+  struct Raw1 {
+    T a, q;
+  };
+  __device__ __forceinline__ Raw1 raw1(int i) const { return Raw1{r[i], pp[i]}; }
+  __device__ __forceinline__ T form1(const Raw1 &w) const { return w.a + beta * w.q; }
 };
 // Mode 4's boundary rows of a partitioned matrix (k_spmv_fd_bnd): own
 // columns form p_k as GatherP, ghosts (from n on) are the neighbours' formed
@@ -1901,6 +1913,10 @@ __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, E
 // value codes. The class bytes of 256 steps come in one dword per lane and
 // are read with v_readlane: no scalar load per slice waits on the memory
 // behind the constant cache.
+#ifndef CGX_LEAN_FULL
+#define CGX_LEAN_FULL 1
+#endif
+constexpr bool LEAN_FULL = CGX_LEAN_FULL;  // (A/B builds: -DCGX_LEAN_FULL=0)
 template <typename T, class Epi, class Gather>
 __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi &epi,
                                           const T *__restrict__ vd,
@@ -2003,27 +2019,44 @@ __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi
     const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
     epi.pre2c(r0, r0 + 1, ct.x, ct.y);
     T a0 = T(0), a1 = T(0);
-    if (pres & 1) {
+    if (LEAN_FULL && pres == 15) {  // every slot present (the interior): no select
       a0 = a0 + v[0] * gmD.x;
       a1 = a1 + v[0] * gmD.y;
-    }
-    if (pres & 2) {
       a0 = a0 + v[1] * gma.x;
       a1 = a1 + v[1] * gma.y;
-    }
-    a0 = a0 + v[2] * left;
-    a1 = a1 + v[2] * ct.x;
-    a0 = a0 + v[3] * ct.x;
-    a1 = a1 + v[3] * ct.y;
-    a0 = a0 + v[4] * ct.y;
-    a1 = a1 + v[4] * right;
-    if (pres & 4) {
+      a0 = a0 + v[2] * left;
+      a1 = a1 + v[2] * ct.x;
+      a0 = a0 + v[3] * ct.x;
+      a1 = a1 + v[3] * ct.y;
+      a0 = a0 + v[4] * ct.y;
+      a1 = a1 + v[4] * right;
       a0 = a0 + v[5] * gpa.x;
       a1 = a1 + v[5] * gpa.y;
-    }
-    if (pres & 8) {
       a0 = a0 + v[6] * gpD.x;
       a1 = a1 + v[6] * gpD.y;
+    } else {
+      if (pres & 1) {
+        a0 = a0 + v[0] * gmD.x;
+        a1 = a1 + v[0] * gmD.y;
+      }
+      if (pres & 2) {
+        a0 = a0 + v[1] * gma.x;
+        a1 = a1 + v[1] * gma.y;
+      }
+      a0 = a0 + v[2] * left;
+      a1 = a1 + v[2] * ct.x;
+      a0 = a0 + v[3] * ct.x;
+      a1 = a1 + v[3] * ct.y;
+      a0 = a0 + v[4] * ct.y;
+      a1 = a1 + v[4] * right;
+      if (pres & 4) {
+        a0 = a0 + v[5] * gpa.x;
+        a1 = a1 + v[5] * gpa.y;
+      }
+      if (pres & 8) {
+        a0 = a0 + v[6] * gpD.x;
+        a1 = a1 + v[6] * gpD.y;
+      }
     }
     epi.row2(r0, a0, a1, true, true);
   }
@@ -2487,6 +2520,53 @@ template <typename T> struct EpiDotOnly {
     pv1 = p[i1];
   }
   __device__ __forceinline__ void row2(int, T s0, T s1, bool l0, bool l1) {
+#ifdef CGX_EXPERIMENT_PLAIN_DOT  // (a measurement build only: not the engine's numerics)
+    acc.hi = acc.hi + s0 * pv;
+    acc.hi = acc.hi + s1 * pv1;
+#else
+    if (l0) acc += s0 * pv;
+    if (l1) acc += s1 * pv1;
+#endif
+  }
+};
+// Recomputed-Ap fused body (mode 7), kernel 1: p_k = r + beta p_{k-1}
+// (CG.hpp:418) stored into P[k mod 4] and value2 += helper.p_k with helper =
+// A p_k not stored — kernel 2 forms it again from the stored p_k
+template <typename T> struct EpiFDDot {
+  T *__restrict__ pc;
+  GatherP<T> g;
+  Dd<T> acc;  // p.Ap (double-length)
+  T pv, pv1;
+  __device__ __forceinline__ void pre(int i) { pv = g(i); }
+  __device__ __forceinline__ void pre2c(int, int, T c0, T c1) {
+    pv = c0;
+    pv1 = c1;
+  }
+  __device__ __forceinline__ void row(int i, T s) {
+    pc[i] = pv;
+    acc += s * pv;
+  }
+  __device__ __forceinline__ void pre2(int i0, int i1) {
+    if (i1 == i0 + 1) {
+      const auto v = g.pair(i0);
+      pv = v.x;
+      pv1 = v.y;
+    } else {
+      pv = g(i0);
+      pv1 = g(i1);
+    }
+  }
+  __device__ __forceinline__ void row2(int i, T s0, T s1, bool l0, bool l1) {
+    using PV = typename PairOf<T>::V;
+    if (l0 && l1 && (((uintptr_t)(pc + i)) & (sizeof(PV) - 1)) == 0) {
+      PV q;
+      q.x = pv;
+      q.y = pv1;
+      *reinterpret_cast<PV *>(pc + i) = q;
+    } else {
+      if (l0) pc[i] = pv;
+      if (l1) pc[i + 1] = pv1;
+    }
     if (l0) acc += s0 * pv;
     if (l1) acc += s1 * pv1;
   }
@@ -2690,6 +2770,377 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean_updr(CsrArgs A, const T *_
     st->pAp[slot] = pAp;
     st->alpha[slot] = alpha;
     st->skip[slot] = 0;
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiUpdR<T> e{r, alpha, T(0), T(0), T(0)};
+  spmv_lean<T>(A, GatherX<T>{p}, e, vd, vt);
+  store_part(ws->rr_part, blockIdx.x, e.acc, sm.red);
+}
+
+// Lane l's value of v for every lane (l uniform)
+template <typename T> __device__ __forceinline__ T lane_bcast(T v, int l);
+template <> __device__ __forceinline__ double lane_bcast(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+template <> __device__ __forceinline__ float lane_bcast(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Tile form of the lean walk (lean_tile_ok; DESIGN.md §4 "tile walk"): one
+// wave walks Y consecutive walk positions of the class layout (Y slices of
+// a plane: Y / M x-lines when a = 128 M rows) through its XCD group's planes,
+// with the planes it needs DIST steps ahead already in flight. The 4-wave
+// walk has one slice's loads in flight per wave (1 KB of HBM lines at 4
+// waves per SIMD, 112 VGPRs: no room for a second set) and waits a memory
+// round trip every step; here a slot of the ring holds a plane's Y center
+// pairs, the +-a pairs from outside the tile and the x-line edge values, and
+// a step sums plane i from slots i - 1, i, i + 1 while planes i + 2 ..
+// i + 1 + DIST are on their way (one wave per SIMD, its VGPRs to spare).
+// Inside the tile the +-a neighbours (k +- M) and the x-line neighbours of
+// the slices' end rows are other slices' centers, read from registers. Per
+// row the same products in the same order as spmv_lean: Ap bit for bit.
+template <typename T, int Y, int M, int DIST, bool REV, class Epi, class Gather>
+__device__ __forceinline__ void spmv_lean_tile(const CsrArgs &A, const Gather &x, Epi &epi,
+                                               const T *__restrict__ vd,
+                                               const unsigned long long *vt, int zs) {
+  constexpr int VG = 8192 | 32768 | 262144 | 524288 | kVT | 2;  // the generic slices' form
+  constexpr int NRC = DIST + 3;                 // center ring: planes i - 1 .. i + 1 + DIST
+  constexpr int U = NRC % 2 ? 2 * NRC : NRC;    // unroll: both rings return to slot 0
+  constexpr int NE = M < Y ? M : Y;             // outside +-a pairs per side
+  using PV = decltype(x.pair_b(0u));
+  using Raw = typename Gather::Raw;    // a pair's loads (GatherP: r's and p_{k-1}'s)
+  using Raw1 = typename Gather::Raw1;
+  // a formed pair kept in a Raw slot (GatherP: in its a half) and read back
+  auto to_raw = [](const PV &v) {
+    Raw w;
+    if constexpr (std::is_same<Raw, PV>::value) w = v;
+    else w.a = v;
+    return w;
+  };
+  auto formed = [](const Raw &w) -> PV {
+    if constexpr (std::is_same<Raw, PV>::value) return w;
+    else return w.a;
+  };
+  struct CSlot {
+    Raw c[Y];  // the plane's center pairs (formed in place the step before their first use)
+  };
+  struct ESlot {  // (two slots: plane i's, plane i + 1's)
+    Raw em[NE];   // -a pairs of slices 0 .. NE - 1 (outside the tile)
+    Raw ep[NE];   // +a pairs of slices Y - NE .. Y - 1
+    Raw1 e;       // lane 0: row fr0 - 1; lane 63: row fr0 + 128 Y (the tile's x-line edges)
+  };
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // workgroup b: XCD group g = b mod 8, tile t of the plane, part zp of the
+  // group's planes (zs parts: more waves per SIMD)
+  const int b = (int)blockIdx.x, g = b & 7;
+  const int tpg = (int)gridDim.x / (8 * zs);  // tiles of workgroups per plane
+  const int step = tpg * 4 * Y;               // walk positions per plane (the layout's)
+  const int t = (b >> 3) % tpg, zp = (b >> 3) / tpg;
+  const int q0 = (t * 4 + wid) * Y;
+  const int nsl = (int)A.nsl;
+  const int lo = (int)(((int64_t)nsl * g) >> 3), end = (int)(((int64_t)nsl * (g + 1)) >> 3);
+  const int J = (end - lo) / step;  // planes of the group (<= 256: one class word per lane)
+  const int ib = zp * J / zs, ie = (zp + 1) * J / zs;  // this wave's walk indices
+  const int nw = A.vl_nst >> 2;
+  const auto *tab = (const __attribute__((address_space(4))) VlClass *)A.vl_tab;
+  const int a = A.vl_a, nxi = (int)A.nx;
+  const unsigned oa = (unsigned)a * (unsigned)sizeof(T);
+  unsigned cw[Y];
+#pragma unroll
+  for (int k = 0; k < Y; ++k) {
+    const unsigned *__restrict__ row = reinterpret_cast<const unsigned *>(
+        A.vl_cls + (int64_t)(g * step + q0 + k) * A.vl_nst);
+    const unsigned w = row[lane < nw ? lane : 0];  // (every lane loads: a fixed load count)
+    cw[k] = lane < nw ? w : ~0u;
+  }
+  // walk index i: plane lo / step + (rev ? J - 1 - i : i); indices -1 and J
+  // are the neighbouring groups' planes (or, at the matrix's ends, clamped to
+  // an in-bounds slice whose pairs the class marks absent)
+  auto first_row = [&](int i) {
+    const int j = REV ? J - 1 - i : i;
+    const int s0 = lo + q0 + j * step;
+    return ((s0 < 0 || s0 + Y > nsl) ? lo + q0 : s0) * (2 * kSellRows);
+  };
+  auto load_c = [&](int i, CSlot &sl) {
+    const int fr0 = first_row(i);
+#pragma unroll
+    for (int k = 0; k < Y; ++k)
+      sl.c[k] = x.raw_b((unsigned)(fr0 + k * 2 * kSellRows + 2 * lane) * (unsigned)sizeof(T));
+  };
+  auto load_e = [&](int i, ESlot &sl) {
+    const int fr0 = first_row(i);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int fr = fr0 + k * 2 * kSellRows;
+      const unsigned rb = (unsigned)(fr + 2 * lane) * (unsigned)sizeof(T);
+      sl.em[k] = x.raw_b(rb - (a > 0 && fr >= a ? oa : 0u));
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int fr = fr0 + (Y - NE + k) * 2 * kSellRows;
+      const unsigned rb = (unsigned)(fr + 2 * lane) * (unsigned)sizeof(T);
+      sl.ep[k] = x.raw_b(rb + (a > 0 && fr + 2 * kSellRows + a <= nxi ? oa : 0u));
+    }
+    const int elo = fr0 > 0 ? fr0 - 1 : 0;
+    const int ehi = fr0 + Y * 2 * kSellRows < nxi ? fr0 + Y * 2 * kSellRows : nxi - 1;
+    sl.e = x.raw1(lane == 0 ? elo : lane == 63 ? ehi : fr0 + 2 * lane);
+  };
+  // plane i's sums: behind / center / ahead in walk order (-D / +D swap in
+  // the reversed sweep)
+  // the centers of the plane a step ahead of the sums, formed (GatherP: p_k
+  // = r + beta p_{k-1}, once per pair; GatherX: the loaded pair)
+  auto form_c = [&](CSlot &sl) {
+#pragma unroll
+    for (int k = 0; k < Y; ++k) sl.c[k] = to_raw(x.form(sl.c[k]));
+  };
+  auto sum = [&](int i, const CSlot &sb, const CSlot &sc, const CSlot &sa, const ESlot &se) {
+    const int j = REV ? J - 1 - i : i;
+    const int s0 = lo + q0 + j * step;
+    const int jb = j >> 2, jsh = 8 * (j & 3);  // plane j's class byte (the forward rows)
+#pragma unroll
+    for (int k = 0; k < Y; ++k) {
+      const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw[k], jb);
+      const int c = (int)((word >> jsh) & 0xffu);
+      const int si = s0 + k;
+      if (c >= 0xfe) continue;  // the generic slices run after the walk
+      const int fr = si * (2 * kSellRows);
+      const int r0 = fr + 2 * lane;
+      const PV ct = formed(sc.c[k]);
+      const PV gmD = formed(REV ? sa.c[k] : sb.c[k]);
+      const PV gpD = formed(REV ? sb.c[k] : sa.c[k]);
+      PV gma, gpa;
+      if (k >= M) gma = formed(sc.c[k >= M ? k - M : 0]);
+      else gma = x.form(se.em[k < NE ? k : 0]);
+      if (k + M < Y) gpa = formed(sc.c[k + M < Y ? k + M : 0]);
+      else gpa = x.form(se.ep[k - (Y - NE) >= 0 ? k - (Y - NE) : 0]);
+      const int pres = tab[c].pres;
+      T v[7];
+#pragma unroll
+      for (int q = 0; q < 7; ++q) v[q] = T(tab[c].v[q]);
+      const T e_f = (k == 0 || k == Y - 1) ? x.form1(se.e) : T(0);
+      const T elo = k == 0 ? e_f : lane_bcast(formed(sc.c[k > 0 ? k - 1 : 0]).y, 63);
+      const T ehi = k == Y - 1 ? e_f : lane_bcast(formed(sc.c[k + 1 < Y ? k + 1 : 0]).x, 0);
+      const T lo_e = tab[c].plo ? elo : -__builtin_copysign(T(0), v[2]);
+      const T hi_e = tab[c].phi ? ehi : -__builtin_copysign(T(0), v[4]);
+      const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
+      epi.pre2c(r0, r0 + 1, ct.x, ct.y);
+      T a0 = T(0), a1 = T(0);
+      if (pres == 15) {  // every slot present (the interior): no select
+        a0 = a0 + v[0] * gmD.x;
+        a1 = a1 + v[0] * gmD.y;
+        a0 = a0 + v[1] * gma.x;
+        a1 = a1 + v[1] * gma.y;
+        a0 = a0 + v[2] * left;
+        a1 = a1 + v[2] * ct.x;
+        a0 = a0 + v[3] * ct.x;
+        a1 = a1 + v[3] * ct.y;
+        a0 = a0 + v[4] * ct.y;
+        a1 = a1 + v[4] * right;
+        a0 = a0 + v[5] * gpa.x;
+        a1 = a1 + v[5] * gpa.y;
+        a0 = a0 + v[6] * gpD.x;
+        a1 = a1 + v[6] * gpD.y;
+      } else {
+        if (pres & 1) {
+          a0 = a0 + v[0] * gmD.x;
+          a1 = a1 + v[0] * gmD.y;
+        }
+        if (pres & 2) {
+          a0 = a0 + v[1] * gma.x;
+          a1 = a1 + v[1] * gma.y;
+        }
+        a0 = a0 + v[2] * left;
+        a1 = a1 + v[2] * ct.x;
+        a0 = a0 + v[3] * ct.x;
+        a1 = a1 + v[3] * ct.y;
+        a0 = a0 + v[4] * ct.y;
+        a1 = a1 + v[4] * right;
+        if (pres & 4) {
+          a0 = a0 + v[5] * gpa.x;
+          a1 = a1 + v[5] * gpa.y;
+        }
+        if (pres & 8) {
+          a0 = a0 + v[6] * gpD.x;
+          a1 = a1 + v[6] * gpD.y;
+        }
+      }
+      epi.row2(r0, a0, a1, true, true);
+    }
+  };
+  CSlot cr[NRC];
+  ESlot er[2];
+  // prologue: walk indices ib - 1 .. ib + DIST + 1 in center slots 0 .. NRC - 1
+  // (index ib + i in slot (i + 1) mod NRC), ib and ib + 1's outside pairs
+#pragma unroll
+  for (int u = 0; u < NRC; ++u) load_c(ib + u - 1, cr[u]);
+  load_e(ib, er[0]);
+  load_e(ib + 1, er[1]);
+  form_c(cr[0]);  // planes ib - 1 and ib; plane i + 1 at step i
+  form_c(cr[1]);
+  // step i (u = i - ib): sums from center slots u, u + 1, u + 2 (mod NRC) and
+  // outside slot u mod 2, then plane i + 2 + DIST into center slot u (the one
+  // plane i - 1 held) and plane i + 2's outside pairs into slot u mod 2.
+  // Unrolled so every slot keeps its registers (no copy of a register with a
+  // load in flight); the loads are never skipped (past the walk's end they
+  // re-read an in-bounds plane), so every path issues the same loads and the
+  // waits count only what a step needs
+  for (int i0 = ib; i0 < ie; i0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u;
+      form_c(cr[(u + 2) % NRC]);
+      if (i < ie) sum(i, cr[u % NRC], cr[(u + 1) % NRC], cr[(u + 2) % NRC], er[u % 2]);
+      load_c(i + 2 + DIST, cr[u % NRC]);
+      load_e(i + 2, er[u % 2]);
+    }
+  }
+  // the slices of other patterns (class 0xff: boundary lines and planes of
+  // another pattern, chunks no template matched), one inlined copy of the
+  // per-slice form for them all
+  for (int i = ib; i < ie; ++i) {
+    const int j = REV ? J - 1 - i : i;
+#pragma unroll
+    for (int k = 0; k < Y; ++k) {
+      const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw[k], j >> 2);
+      if (((word >> (8 * (j & 3))) & 0xffu) == 0xff)
+        sellpv_slice2<T, VG, Epi, Gather>(A, x, epi, vd, lo + q0 + j * step + k, vt);
+    }
+  }
+}
+
+// Mode 6's kernel 1 in the tile walk (lean_tile_ok): k_spmv_lean_dot's
+// values; kTileZ parts of each group's planes, kTileW waves per SIMD
+#ifndef CGX_TILE_Y
+#define CGX_TILE_Y 2
+#endif
+#ifndef CGX_TILE_Z
+#define CGX_TILE_Z 2
+#endif
+#ifndef CGX_TILE_DIST
+#define CGX_TILE_DIST 1
+#endif
+constexpr int kTileY = CGX_TILE_Y, kTileM = 2, kTileDist = CGX_TILE_DIST, kTileZ = CGX_TILE_Z;
+constexpr int kTileW = 4 * kTileZ / kTileY;  // waves per SIMD at the 1,024-workgroup layout
+template <typename T>
+__global__ __launch_bounds__(kBlock, kTileW) void k_spmv_lean_dot_tile(CsrArgs A,
+                                                                       const T *__restrict__ p,
+                                                                       CgScalars<T> *st, int slot,
+                                                                       RedWs<T> *ws) {
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiDotOnly<T> e{p, T(0), T(0), T(0)};
+  if (A.rev)  // (a template: the +-D roles swap without a select per pair)
+    spmv_lean_tile<T, kTileY, kTileM, kTileDist, true>(A, GatherX<T>{p}, e, vd, vt, kTileZ);
+  else
+    spmv_lean_tile<T, kTileY, kTileM, kTileDist, false>(A, GatherX<T>{p}, e, vd, vt, kTileZ);
+  store_part(ws->pap_part, blockIdx.x, e.acc, sm.red);
+}
+
+// Mode 7 (cgx_abi.cpp enqueue_iter_fdefer), kernel 1 of 2 (3 in slot 3):
+// k_spmv_fd_lean's preamble (beta from body k-1's r.r partials, the records,
+// slot 0 opening a group) and its p_k = r + beta p_{k-1} into P[s], in the
+// tile walk: the ring's center pairs are formed once, a step before their
+// first use, and serve as the -D / center / +D and in-tile +-a pairs; only
+// the tile's outside +-a pairs and x-line edges are formed where used. No Ap
+// vector: p.Ap partials only (kernel 2 forms A p_k again).
+// (its ring holds two pairs per position, r's and p_{k-1}'s: kFdZ parts,
+// kFdW waves per SIMD; at four waves it spilled)
+#ifndef CGX_FD_Z
+#define CGX_FD_Z 1
+#endif
+#ifndef CGX_FD_DIST
+#define CGX_FD_DIST 1
+#endif
+constexpr int kFdZ = CGX_FD_Z, kFdDist = CGX_FD_DIST, kFdW = 4 * kFdZ / kTileY;
+template <typename T>
+__global__ __launch_bounds__(kBlock, kFdW) void k_spmv_fd_dot_tile(
+    CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
+    CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr) {
+  __shared__ SellLds<T> sm;
+  const int prev = (slot + 3) & 3;
+  const long long bodies = st->bodies;
+  const bool act = st->active[slot] != 0;
+  if (slot == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int t = 0; t < 4; ++t) st->ran[t] = 0;
+  if (!act) {
+    if (blockIdx.x == 0 && bodies > 0 && (int)(bodies & 3) == slot) {
+      const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+      if (threadIdx.x == 0) {
+        st->rr[prev] = rr;
+        st->rxr[slot] = rr;
+      }
+    }
+    return;
+  }
+  T beta = T(0);
+  if (bodies > 0) {
+    const T rr = sum_parts(ws->rr_part, np_rr, sm.red);
+    beta = rr / st->rxr[prev];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->rr[prev] = rr;  // the record
+      st->rxr[slot] = rr;
+    }
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  const GatherP<T> g{r, pold, beta};
+  EpiFDDot<T> e{pc, g, T(0), T(0), T(0)};
+  if (A.rev)
+    spmv_lean_tile<T, kTileY, kTileM, kFdDist, true>(A, g, e, vd, vt, kFdZ);
+  else
+    spmv_lean_tile<T, kTileY, kTileM, kFdDist, false>(A, g, e, vd, vt, kFdZ);
+  store_part(ws->pap_part, blockIdx.x, e.acc, sm.red);
+}
+
+// Mode 7, kernel 2: k_spmv_lean_updr on the stored p_k with update_r's stop
+// rule (the r.r the body started with, which kernel 1 recorded; bodies, the
+// next slot's active flag, ran[slot]) — mode 4's kernel 2 with A p_k formed
+// again instead of read
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_lean_updr_rule(CsrArgs A,
+                                                                const T *__restrict__ p,
+                                                                T *__restrict__ r,
+                                                                CgScalars<T> *st, int slot,
+                                                                RedWs<T> *ws, int np_pap) {
+  if (!st->active[slot]) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->active[(slot + 1) & 3] = 0;
+    return;
+  }
+  __shared__ SellLds<T> sm;
+  const T pAp = sum_parts(ws->pap_part, np_pap, sm.red);
+  const T rxr = st->rxr[slot];
+  const T alpha = rxr / pAp;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->pAp[slot] = pAp;
+    st->alpha[slot] = alpha;
+    st->skip[slot] = 0;
+    const long long m = st->bodies + 1;  // stop rule, as k_update_xp
+    st->bodies = m;
+    const bool cond = isnan(rxr) || sqrt(rxr) <= st->tol;
+    const bool cont = !cond && m < st->cap;
+    st->active[(slot + 1) & 3] = cont ? 1 : 0;
+    st->stopped = cond ? 1 : (cont ? 0 : 2);
+    st->ran[slot] = 1;
   }
   const T *vd = static_cast<const T *>(A.svdict);
   const unsigned long long *vt = A.vct;
@@ -4400,6 +4851,26 @@ hipError_t Launch<T>::cg_init(const CsrDev &A, const T *x, const T *b, T *r, T *
                               hipStream_t s) {
   CGX_CSR_ONEOFF(k_cg_init, args(A), (const T *)A.val, x, b, r, p, st, ws, tol, cap);
 }
+// The tile walk (spmv_lean_tile) takes the lean layout when it is the
+// plane-per-step carry walk of a 3-D stencil with a = 2 slices, every XCD
+// group whole planes (<= 256 of them) and a plane's positions whole tiles;
+// $CGX_LEAN_TILE=0 keeps the 4-wave walk
+bool lean_tile_ok(const CsrDev &A) {
+  static const int env = [] {
+    const char *e = getenv("CGX_LEAN_TILE");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || !vl_whole(A) || A.vl_P != 0 || A.vl_a != kTileM * 2 * kSellRows) return false;
+  const int64_t step = A.vl_grid / 2;
+  if (step <= 0 || A.vl_D != step * 2 * kSellRows || step % (4 * kTileY)) return false;
+  if (A.nsl % 8 || (A.nsl / 8) % step || (A.nsl / 8) / step > 256) return false;
+  return true;
+}
+// p.Ap partials of mode 6's kernel 1: one per workgroup of its launch
+int lean_dot_parts(const CsrDev &A) {
+  return lean_tile_ok(A) ? A.vl_grid / kTileY * kTileZ : A.vl_grid;  // 8 step kTileZ / (4 Y)
+}
+int fd_dot_parts(const CsrDev &A) { return A.vl_grid / kTileY * kFdZ; }
 template <typename T> int Launch<T>::lean_resident() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> workgroups
@@ -4443,7 +4914,33 @@ hipError_t Launch<T>::lean_dot(const CsrDev &A, const T *p, CgScalars<T> *st, in
   if (!vl_whole(A)) return hipErrorInvalidValue;
   CsrArgs a = args(A);
   a.rev = rev;
+  if (lean_tile_ok(A)) {
+    CGX_GGL(k_spmv_lean_dot_tile<T>, dim3(lean_dot_parts(A)), dim3(kBlock), 0, s, a, p, st,
+            slot, ws);
+    return hipGetLastError();
+  }
   CGX_GGL(k_spmv_lean_dot<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, st, slot, ws);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t Launch<T>::fd_dot_tile(const CsrDev &A, const T *r, const T *pold, T *pc,
+                                  CgScalars<T> *st, int slot, RedWs<T> *ws, int np_rr,
+                                  hipStream_t s, int rev) {
+  if (!lean_tile_ok(A)) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  CGX_GGL(k_spmv_fd_dot_tile<T>, dim3(fd_dot_parts(A)), dim3(kBlock), 0, s, a, r, pold, pc, st,
+          slot, ws, np_rr);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t Launch<T>::lean_updr_rule(const CsrDev &A, const T *p, T *r, CgScalars<T> *st,
+                                     int slot, RedWs<T> *ws, hipStream_t s, int rev) {
+  if (!lean_tile_ok(A)) return hipErrorInvalidValue;
+  CsrArgs a = args(A);
+  a.rev = rev;
+  CGX_GGL(k_spmv_lean_updr_rule<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, r, st, slot, ws,
+          fd_dot_parts(A));
   return hipGetLastError();
 }
 template <typename T>
@@ -4453,7 +4950,7 @@ hipError_t Launch<T>::lean_updr(const CsrDev &A, const T *p, T *r, CgScalars<T> 
   CsrArgs a = args(A);
   a.rev = rev;
   CGX_GGL(k_spmv_lean_updr<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, r, st, slot, ws,
-          A.vl_grid);
+          lean_dot_parts(A));
   return hipGetLastError();
 }
 template <typename T>

@@ -270,7 +270,12 @@ int cgx_cg_config(cgx_cg *cg, int poll_every, int use_graph);
  * Mode 6 (round 6; single device, the lean stencil walk): mode 3's body with
  * no Ap vector — kernel 1 walks A p keeping only p.Ap, kernel 2 walks A p
  * again and updates r in its epilogue (8 N bytes written and read less).
- * The dots are double-length sums (round 6), so modes 1, 3, 4 and 6 give
+ * Mode 7 (single device, f64, a 3-D stencil whose lean layout takes the tile
+ * walk): mode 4's body with no Ap vector — kernel 1 forms p_k into the p ring
+ * and keeps p.Ap, kernel 2 walks A p_k again, updates r and runs the stop
+ * rule, slot 3 adds the x flush launch (60 N + 2 x matrix bytes per body);
+ * never auto (slower than mode 6 at 256^3).
+ * The dots are double-length sums (round 6), so modes 1, 3, 4, 6 and 7 give
  * bit-identical x whatever their grids. */
 int cgx_cg_set_mode(cgx_cg *cg, int mode);
 /* mode 5's launch shape: rows per thread, threads per workgroup (1024),

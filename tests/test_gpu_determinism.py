@@ -85,10 +85,11 @@ def test_256cubed_every_form_and_mode_bit_identical_to_dd_oracle(queue, oracle):
     want, _ = oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=16, max_iter=BODIES)
     m = cga.Matrix.poisson(queue, 3, 256, 256, 256)
     forms = _forms(m, extra=(15 | KIL,))
-    # the production form (the lean walk) in modes 1, 3, 4 and 6 (Ap recomputed
-    # by a second walk instead of stored); the rest in mode 3
+    # the production form (the lean walk) in modes 1, 3, 4, 6 (Ap recomputed
+    # by a second walk instead of stored) and 7 (mode 4's formed p_k with Ap
+    # recomputed, the tile walk); the rest in mode 3
     assert _variant(m) & KVL
-    ran = _check_forms(queue, m, b, want, [_variant(m)], modes=(1, 3, 4, 6))
+    ran = _check_forms(queue, m, b, want, [_variant(m)], modes=(1, 3, 4, 6, 7))
     ran += _check_forms(queue, m, b, want, [v for v in forms if not v & KVL])
     print("256^3 forms x modes, x bit-identical to the dd oracle:", ran)
     assert len(ran) >= 8, ran  # CSR-stream, SELL, SELL-P, value codes, templates, lean
@@ -106,6 +107,21 @@ def test_256cubed_stop_rule_bodies_exact(queue, oracle):
     m = cga.Matrix.poisson(queue, 3, 256, 256, 256)
     x, it = _solve(queue, m, b, 0, bodies=-1, tol=tol)
     assert res.stopped_by_tol
+    assert it == res.iterations
+    assert np.array_equal(x, want), float(np.max(np.abs(x - want)))
+
+
+@pytest.mark.parametrize("mode", [6, 7])
+def test_256cubed_stop_rule_bodies_exact_recomputed(queue, oracle, mode):
+    """Modes 6 and 7 to tolerance: the same bodies and x as the dd oracle
+    (mode 7's stop rule runs in its kernel 2, as mode 4's update_r)."""
+    rp, cl, vl = oracle.poisson(3, 256, 256, 256)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)
+    tol = 1e-8 * float(np.linalg.norm(b))
+    want, res = oracle.cg_solve_dd(rp, cl, vl, b, tol, threads=16)
+    m = cga.Matrix.poisson(queue, 3, 256, 256, 256)
+    x, it = _solve(queue, m, b, mode, bodies=-1, tol=tol)
     assert it == res.iterations
     assert np.array_equal(x, want), float(np.max(np.abs(x - want)))
 
