@@ -368,8 +368,8 @@ template <typename T> int enqueue_iter_defer(cgx_cg *cg, int slot) {
          })))
       return rc;
     return timed(cg, 3, s, [&] {
-      return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws, A->dev.vl_grid, s,
-                                       par, nullptr);
+      return Launch<T>::update_p_defer(cg->n, x, p, pn, P, r, st, slot, ws,
+                                       lean_updr_parts(A->dev), s, par, nullptr);
     });
   }
   if ((rc = enqueue_spmv_dot<T>(cg, p, slot, par, &npp))) return rc;

@@ -251,6 +251,8 @@ __host__ __device__ inline bool vl_whole(const CsrDev &A) {
 bool lean_tile_ok(const CsrDev &A);
 int lean_dot_parts(const CsrDev &A);
 int fd_dot_parts(const CsrDev &A);  // mode 7's kernel 1 (lean_tile_ok)
+int lean_updr_parts(const CsrDev &A);  // mode 6's kernel 2
+bool lean_updr_tile(const CsrDev &A);
 
 // Kernel-execution timing (cgx_abi.cpp timed(), kernel timing on): the next
 // launch takes these start / stop events, recorded by its dispatch itself

@@ -2783,6 +2783,30 @@ __global__ __launch_bounds__(kBlock) void k_spmv_lean_updr(CsrArgs A, const T *_
   store_part(ws->rr_part, blockIdx.x, e.acc, sm.red);
 }
 
+// The tile walk's prefetch of an epilogue's own rows: none by default;
+// EpiUpdRT's r pairs come with the plane's outside pairs, two steps early
+struct NoPre {};
+template <class Epi> struct EpiPre {
+  using type = NoPre;
+  __device__ __forceinline__ static NoPre fetch(const Epi &, int) { return NoPre{}; }
+  __device__ __forceinline__ static void take(Epi &, const NoPre &) {}
+};
+// Mode 6's kernel 2 in the tile walk: EpiUpdR with r's pair prefetched
+// (pre2c loads nothing; the generic slices' pre / pre2 load as EpiUpdR)
+template <typename T> struct EpiUpdRT : EpiUpdR<T> {
+  __device__ __forceinline__ void pre2c(int, int, T, T) {}
+};
+template <typename T> struct EpiPre<EpiUpdRT<T>> {
+  using type = typename PairOf<T>::V;
+  __device__ __forceinline__ static type fetch(const EpiUpdRT<T> &e, int r0) {
+    return *reinterpret_cast<const type *>(e.r + r0);
+  }
+  __device__ __forceinline__ static void take(EpiUpdRT<T> &e, const type &v) {
+    e.rv = v.x;
+    e.rv1 = v.y;
+  }
+};
+
 // Lane l's value of v for every lane (l uniform)
 template <typename T> __device__ __forceinline__ T lane_bcast(T v, int l);
 template <> __device__ __forceinline__ double lane_bcast(double v, int l) {
@@ -2831,10 +2855,12 @@ __device__ __forceinline__ void spmv_lean_tile(const CsrArgs &A, const Gather &x
   struct CSlot {
     Raw c[Y];  // the plane's center pairs (formed in place the step before their first use)
   };
+  using Pre = typename EpiPre<Epi>::type;  // the epilogue's own rows (EpiUpdRT: r's pairs)
   struct ESlot {  // (two slots: plane i's, plane i + 1's)
     Raw em[NE];   // -a pairs of slices 0 .. NE - 1 (outside the tile)
     Raw ep[NE];   // +a pairs of slices Y - NE .. Y - 1
     Raw1 e;       // lane 0: row fr0 - 1; lane 63: row fr0 + 128 Y (the tile's x-line edges)
+    Pre pre[Y];
   };
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2892,6 +2918,8 @@ __device__ __forceinline__ void spmv_lean_tile(const CsrArgs &A, const Gather &x
     const int elo = fr0 > 0 ? fr0 - 1 : 0;
     const int ehi = fr0 + Y * 2 * kSellRows < nxi ? fr0 + Y * 2 * kSellRows : nxi - 1;
     sl.e = x.raw1(lane == 0 ? elo : lane == 63 ? ehi : fr0 + 2 * lane);
+#pragma unroll
+    for (int k = 0; k < Y; ++k) sl.pre[k] = EpiPre<Epi>::fetch(epi, fr0 + k * 2 * kSellRows + 2 * lane);
   };
   // plane i's sums: behind / center / ahead in walk order (-D / +D swap in
   // the reversed sweep)
@@ -2932,6 +2960,7 @@ __device__ __forceinline__ void spmv_lean_tile(const CsrArgs &A, const Gather &x
       const T hi_e = tab[c].phi ? ehi : -__builtin_copysign(T(0), v[4]);
       const T left = wave_shr1(ct.y, lo_e), right = wave_shl1(ct.x, hi_e);
       epi.pre2c(r0, r0 + 1, ct.x, ct.y);
+      EpiPre<Epi>::take(epi, se.pre[k]);
       T a0 = T(0), a1 = T(0);
       if (pres == 15) {  // every slot present (the interior): no select
         a0 = a0 + v[0] * gmD.x;
@@ -3049,6 +3078,41 @@ __global__ __launch_bounds__(kBlock, kTileW) void k_spmv_lean_dot_tile(CsrArgs A
   else
     spmv_lean_tile<T, kTileY, kTileM, kTileDist, false>(A, GatherX<T>{p}, e, vd, vt, kTileZ);
   store_part(ws->pap_part, blockIdx.x, e.acc, sm.red);
+}
+
+// Mode 6's kernel 2 in the tile walk (lean_tile_ok): k_spmv_lean_updr's
+// values, r's pairs prefetched with the planes
+template <typename T>
+__global__ __launch_bounds__(kBlock, kTileW) void k_spmv_lean_updr_tile(CsrArgs A,
+                                                                        const T *__restrict__ p,
+                                                                        T *__restrict__ r,
+                                                                        CgScalars<T> *st, int slot,
+                                                                        RedWs<T> *ws, int np_pap) {
+  if (!st->active[slot]) return;
+  __shared__ SellLds<T> sm;
+  const T pAp = sum_parts(ws->pap_part, np_pap, sm.red);
+  const T alpha = st->rxr[slot] / pAp;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->pAp[slot] = pAp;
+    st->alpha[slot] = alpha;
+    st->skip[slot] = 0;
+  }
+  const T *vd = static_cast<const T *>(A.svdict);
+  const unsigned long long *vt = A.vct;
+  if (A.vl_lds) {
+    lean_lds(A, sm);
+    vd = sm.vdict;
+    vt = sm.vt;
+  }
+  EpiUpdRT<T> e;
+  e.r = r;
+  e.alpha = alpha;
+  e.acc = Dd<T>(T(0));
+  if (A.rev)
+    spmv_lean_tile<T, kTileY, kTileM, kTileDist, true>(A, GatherX<T>{p}, e, vd, vt, kTileZ);
+  else
+    spmv_lean_tile<T, kTileY, kTileM, kTileDist, false>(A, GatherX<T>{p}, e, vd, vt, kTileZ);
+  store_part(ws->rr_part, blockIdx.x, e.acc, sm.red);
 }
 
 // Mode 7 (cgx_abi.cpp enqueue_iter_fdefer), kernel 1 of 2 (3 in slot 3):
@@ -4871,6 +4935,19 @@ int lean_dot_parts(const CsrDev &A) {
   return lean_tile_ok(A) ? A.vl_grid / kTileY * kTileZ : A.vl_grid;  // 8 step kTileZ / (4 Y)
 }
 int fd_dot_parts(const CsrDev &A) { return A.vl_grid / kTileY * kFdZ; }
+// mode 6's kernel 2 in the tile form ($CGX_LEAN_TILE_UPDR=1; with r's pairs
+// prefetched it ran 74.4 against 68.6 us at 256^3, profiles/r6t_*: off by
+// default), and its r.r partials
+bool lean_updr_tile(const CsrDev &A) {
+  static const int env = [] {
+    const char *e = getenv("CGX_LEAN_TILE_UPDR");
+    return e ? atoi(e) : 0;
+  }();
+  return env && lean_tile_ok(A);
+}
+int lean_updr_parts(const CsrDev &A) {
+  return lean_updr_tile(A) ? A.vl_grid / kTileY * kTileZ : A.vl_grid;
+}
 template <typename T> int Launch<T>::lean_resident() {
   static std::mutex mu;
   static std::map<int, int> cache;  // device -> workgroups
@@ -4949,6 +5026,11 @@ hipError_t Launch<T>::lean_updr(const CsrDev &A, const T *p, T *r, CgScalars<T> 
   if (!vl_whole(A)) return hipErrorInvalidValue;
   CsrArgs a = args(A);
   a.rev = rev;
+  if (lean_updr_tile(A)) {
+    CGX_GGL(k_spmv_lean_updr_tile<T>, dim3(lean_updr_parts(A)), dim3(kBlock), 0, s, a, p, r, st,
+            slot, ws, lean_dot_parts(A));
+    return hipGetLastError();
+  }
   CGX_GGL(k_spmv_lean_updr<T>, dim3(A.vl_grid), dim3(kBlock), 0, s, a, p, r, st, slot, ws,
           lean_dot_parts(A));
   return hipGetLastError();
