@@ -124,10 +124,13 @@ def test_g3_standin_spmv_bitexact(queue, oracle, g3):
 def test_g3_standin_fixed_bodies_match_oracle(queue, oracle, g3):
     """Config 5's shape at fixed body counts (tol 0, no stop), the auto
     iteration against the oracle's OpenMP restatement. Its iterates are
-    sensitive to the dots' summation order: the oracle against itself on 16
-    and on 8 threads differs by ~7e-14 after 10 bodies but ~7e-7 after 40
-    (ill-conditioned, shift 1e-2). So: SURVEY §8(c)'s 1e-10 after 10 bodies,
-    and after 40 the GPU within 10x of the oracle's own spread."""
+    sensitive to the dots' summation order: the plain-sum oracle against
+    itself on 16 and on 8 threads differs by ~7e-14 after 10 bodies but by
+    3e-8 .. 7e-7 after 40 (ill-conditioned, shift 1e-2; the OpenMP reduction's
+    combine order is not fixed, so that spread changes from run to run and
+    is no bar). So: SURVEY §8(c)'s 1e-10 after 10 bodies against the plain
+    oracle, and after 40 the oracle's model of the engine's arithmetic
+    (double-length dots, cg_solve_dd) bit for bit."""
     rp, cl, vl = g3
     b = np.arange(1, G3_N + 1, dtype=np.float64)
     m = cga.Matrix(queue, vl, cl, rp)
@@ -140,10 +143,13 @@ def test_g3_standin_fixed_bodies_match_oracle(queue, oracle, g3):
         x = cg.extract()
         _, x16 = oracle.cg_fixed_iters_omp(rp, cl, vl, b, bodies, 16)
         _, x8 = oracle.cg_fixed_iters_omp(rp, cl, vl, b, bodies, 8)
-        spread = rel(x16, x8)
-        print("g3", bodies, "bodies: gpu vs oracle", rel(x, x16), "oracle 16 vs 8 threads", spread)
-        bar = 1e-10 if bodies == 10 else max(1e-10, 10 * spread)
-        assert rel(x, x16) <= bar, (bodies, rel(x, x16), spread)
+        print("g3", bodies, "bodies: gpu vs oracle", rel(x, x16), "oracle 16 vs 8 threads",
+              rel(x16, x8))
+        if bodies == 10:
+            assert rel(x, x16) <= 1e-10, (bodies, rel(x, x16))
+        else:
+            xdd, _ = oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=16, max_iter=bodies)
+            assert np.array_equal(x, xdd), float(np.max(np.abs(x - xdd)))
 
 
 def test_g3_standin_solve_matches_oracle(queue, oracle, g3):
