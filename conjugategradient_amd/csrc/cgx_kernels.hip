@@ -4928,7 +4928,10 @@ bool lean_tile_ok(const CsrDev &A) {
   const int64_t step = A.vl_grid / 2;
   if (step <= 0 || A.vl_D != step * 2 * kSellRows || step % (4 * kTileY)) return false;
   if (A.nsl % 8 || (A.nsl / 8) % step || (A.nsl / 8) / step > 256) return false;
-  return true;
+  // at least 8 planes per wave: a part's two halo planes are loaded again (the
+  // 256 x 256 x 32 slab, 4 planes per XCD group, ran its p.Ap walk in 11.6
+  // against 8.2 us in the 4-wave form, profiles/r6final_slab_*)
+  return (A.nsl / 8) / step >= 8 * kTileZ;
 }
 // p.Ap partials of mode 6's kernel 1: one per workgroup of its launch
 int lean_dot_parts(const CsrDev &A) {
