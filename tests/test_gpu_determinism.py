@@ -111,6 +111,22 @@ def test_256cubed_stop_rule_bodies_exact(queue, oracle):
     assert np.array_equal(x, want), float(np.max(np.abs(x - want)))
 
 
+def test_tile_walk_other_shape_bit_identical_to_dd_oracle(queue, oracle):
+    """The tile walk (modes 6 and 7's p.Ap walk, lean_tile_ok) on a second
+    shape it takes: 256 x 128 x 256 (a = 2 slices, 256 slices per plane, 16
+    planes per wave at two parts per XCD group), x equal to the dd oracle bit
+    for bit in modes 6 and 7, and to mode 3 (the 4-wave walk's body)."""
+    dims = (3, 256, 128, 256)
+    rp, cl, vl = oracle.poisson(*dims)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)
+    want, _ = oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=16, max_iter=BODIES)
+    m = cga.Matrix.poisson(queue, *dims)
+    assert _variant(m) & KVL
+    ran = _check_forms(queue, m, b, want, [_variant(m)], modes=(3, 6, 7))
+    print("256x128x256:", ran)
+
+
 @pytest.mark.parametrize("mode", [6, 7])
 def test_256cubed_stop_rule_bodies_exact_recomputed(queue, oracle, mode):
     """Modes 6 and 7 to tolerance: the same bodies and x as the dd oracle
