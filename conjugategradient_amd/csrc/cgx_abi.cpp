@@ -3227,6 +3227,8 @@ extern "C" int cgx_cg_destroy(cgx_cg *cg) {
   (void)hipStreamSynchronize(cg->ctx->stream);
   drop_graph(cg);
   for (auto e : cg->ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : cg->run_ev)
+    if (e) (void)hipEventDestroy(e);
   for (void *p : {cg->r, cg->p, cg->p2, cg->Ap, cg->st, cg->ws, cg->pk[0], cg->pk[1], cg->pk[2],
                   cg->coop_ws, cg->coop_trace})
     if (p) (void)hipFree(p);
@@ -3340,9 +3342,9 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   if (cg->graph_x != cg->x) drop_graph(cg);
   // Two host staging buffers: chunk c's state is read while chunk c+1 runs.
   auto *hbuf = (char *)cg->ctx->h_pinned;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  CGX_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
-  CGX_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  for (int k = 0; k < 2; ++k)
+    if (!cg->run_ev[k]) CGX_HIP(hipEventCreateWithFlags(&cg->run_ev[k], hipEventDisableTiming));
+  hipEvent_t *ev = cg->run_ev;
   struct Pending { int buf; int slot_after; int64_t iters; };
   std::vector<Pending> q;
   int64_t remaining = bodies;
@@ -3407,8 +3409,6 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
   }
   // drain whatever is still queued
   while (rc == CGX_OK && !q.empty()) rc = wait_one();
-  (void)hipEventDestroy(ev[0]);
-  (void)hipEventDestroy(ev[1]);
   if (rc) return rc;
   if (last_stopped == 3) {
     set_error("peer transport: a device-side wait timed out (a rank stopped responding, or "

@@ -252,6 +252,9 @@ struct cgx_cg {
   // cgx_cg_prepare built ahead of a run; all captured for x = graph_x
   std::map<std::pair<int, int64_t>, hipGraphExec_t> graphs;
   void *graph_x = nullptr;
+  // cgx_cg_run's two poll events, created once (an event create and destroy
+  // per run sat inside every caller's timed region)
+  hipEvent_t run_ev[2] = {nullptr, nullptr};
   // kernel timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
