@@ -1913,10 +1913,9 @@ __device__ __forceinline__ void spmv_sellpv(const CsrArgs &A, const Gather &x, E
 // value codes. The class bytes of 256 steps come in one dword per lane and
 // are read with v_readlane: no scalar load per slice waits on the memory
 // behind the constant cache.
-#ifndef CGX_LEAN_FULL
-#define CGX_LEAN_FULL 1
-#endif
-constexpr bool LEAN_FULL = CGX_LEAN_FULL;  // (A/B builds: -DCGX_LEAN_FULL=0)
+// the select-free interior path of the lean walk (37.3 against 38.5 us for
+// mode 6's p.Ap walk at 256^3 without it, profiles/r6t_*)
+constexpr bool LEAN_FULL = true;
 template <typename T, class Epi, class Gather>
 __device__ __forceinline__ void spmv_lean(const CsrArgs &A, const Gather &x, Epi &epi,
                                           const T *__restrict__ vd,
@@ -2520,13 +2519,8 @@ template <typename T> struct EpiDotOnly {
     pv1 = p[i1];
   }
   __device__ __forceinline__ void row2(int, T s0, T s1, bool l0, bool l1) {
-#ifdef CGX_EXPERIMENT_PLAIN_DOT  // (a measurement build only: not the engine's numerics)
-    acc.hi = acc.hi + s0 * pv;
-    acc.hi = acc.hi + s1 * pv1;
-#else
     if (l0) acc += s0 * pv;
     if (l1) acc += s1 * pv1;
-#endif
   }
 };
 // Recomputed-Ap fused body (mode 7), kernel 1: p_k = r + beta p_{k-1}
@@ -3047,16 +3041,9 @@ __device__ __forceinline__ void spmv_lean_tile(const CsrArgs &A, const Gather &x
 
 // Mode 6's kernel 1 in the tile walk (lean_tile_ok): k_spmv_lean_dot's
 // values; kTileZ parts of each group's planes, kTileW waves per SIMD
-#ifndef CGX_TILE_Y
-#define CGX_TILE_Y 2
-#endif
-#ifndef CGX_TILE_Z
-#define CGX_TILE_Z 2
-#endif
-#ifndef CGX_TILE_DIST
-#define CGX_TILE_DIST 1
-#endif
-constexpr int kTileY = CGX_TILE_Y, kTileM = 2, kTileDist = CGX_TILE_DIST, kTileZ = CGX_TILE_Z;
+// (measured, profiles/r6t_*: Y 2 / Z 2 / DIST 1 35.8 us; DIST 2 42.1; Y 4 Z 4
+// 40.8; Y 4 Z 2 DIST 3, two waves per SIMD, 40.1)
+constexpr int kTileY = 2, kTileM = 2, kTileDist = 1, kTileZ = 2;
 constexpr int kTileW = 4 * kTileZ / kTileY;  // waves per SIMD at the 1,024-workgroup layout
 template <typename T>
 __global__ __launch_bounds__(kBlock, kTileW) void k_spmv_lean_dot_tile(CsrArgs A,
@@ -3124,13 +3111,9 @@ __global__ __launch_bounds__(kBlock, kTileW) void k_spmv_lean_updr_tile(CsrArgs 
 // vector: p.Ap partials only (kernel 2 forms A p_k again).
 // (its ring holds two pairs per position, r's and p_{k-1}'s: kFdZ parts,
 // kFdW waves per SIMD; at four waves it spilled)
-#ifndef CGX_FD_Z
-#define CGX_FD_Z 1
-#endif
-#ifndef CGX_FD_DIST
-#define CGX_FD_DIST 1
-#endif
-constexpr int kFdZ = CGX_FD_Z, kFdDist = CGX_FD_DIST, kFdW = 4 * kFdZ / kTileY;
+// (Z 1 DIST 1: 101 us at 256^3; Z 1 DIST 0 105, Z 1 DIST 2 123, Z 2 DIST 0
+// 111 with a spill; profiles/r6t_*)
+constexpr int kFdZ = 1, kFdDist = 1, kFdW = 4 * kFdZ / kTileY;
 template <typename T>
 __global__ __launch_bounds__(kBlock, kFdW) void k_spmv_fd_dot_tile(
     CsrArgs A, const T *__restrict__ r, const T *__restrict__ pold, T *__restrict__ pc,
