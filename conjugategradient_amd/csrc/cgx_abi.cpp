@@ -3396,10 +3396,13 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
       if ((rc = poll_state(cg, hbuf + 256 * buf, s))) break;
       CGX_HIP(hipEventRecord(ev[buf], s));
       q.push_back(Pending{buf, cg->slot, chunk});
-      if (remaining == 0 && !cg->A->dist && !cg->coop) {
+      if (remaining == 0 && !cg->A->dist && !cg->coop && !(cg->defer && cg->slot == 0)) {
         // the end-of-run x flush reads only device state and the slot, so a
         // single-device run queues it behind its last chunk instead of after
-        // the host has seen that chunk finish (one host round trip less)
+        // the host has seen that chunk finish (one host round trip less).
+        // (Modes 3 / 6 ending at slot 0: the slot-3 body applied the group, so
+        // the flush is needed only if the run stopped inside the group; the
+        // host decides once it has read the state below)
         if ((rc = flush_pending_x(cg))) break;
         flushed = true;
       }
@@ -3420,7 +3423,9 @@ extern "C" int cgx_cg_run(cgx_cg *cg, int64_t bodies, int64_t *bodies_total, int
               "the launch was not resident); the solve was stopped, x is not updated");
     return CGX_EHIP;
   }
-  if (!flushed && (rc = flush_pending_x(cg))) return rc;
+  // (modes 3 / 6 at slot 0 with every body active: the group is applied)
+  const bool applied = cg->defer && cg->slot == 0 && last_stopped == 0 && !cg->A->dist;
+  if (!flushed && !applied && (rc = flush_pending_x(cg))) return rc;
   CGX_HIP(hipStreamSynchronize(s));
   if (cg->timing) {
     CGX_HIP(hipStreamSynchronize(s));
