@@ -127,6 +127,33 @@ def test_tile_walk_other_shape_bit_identical_to_dd_oracle(queue, oracle):
     print("256x128x256:", ran)
 
 
+def test_tile_walk_f32(queue, oracle):
+    """The tile walk in f32 (mode 6's p.Ap kernel, T = float): 20 bodies at
+    256 x 128 x 256 against mode 3 (the 4-wave walk's body) and the f64 dd
+    oracle. f32 dots keep f32 pairs, which are not split-independent (§6),
+    so the bars are tolerances: a wrong neighbour or edge would be far
+    outside them."""
+    dims = (3, 256, 128, 256)
+    rp, cl, vl = oracle.poisson(*dims)
+    n = len(rp) - 1
+    b = np.arange(1, n + 1, dtype=np.float64)
+    want, _ = oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=16, max_iter=20)
+    m = cga.Matrix.poisson(queue, *dims, dtype=np.float32)
+    xs = {}
+    for mode in (3, 6):
+        cg = cga.CG(queue, np.float32)
+        cg.mode = mode
+        cg.setMatrix(m)
+        cg.setTarget(b.astype(np.float32))
+        cg.solve(0.0, max_iter=20)
+        assert cg.iterations == 20
+        xs[mode] = cg.extract().astype(np.float64)
+    d36 = float(np.linalg.norm(xs[6] - xs[3]) / np.linalg.norm(xs[3]))
+    d6 = float(np.linalg.norm(xs[6] - want) / np.linalg.norm(want))
+    print("f32 tile walk: mode 6 vs 3", d36, "vs f64 dd oracle", d6)
+    assert d36 <= 1e-5 and d6 <= 1e-4, (d36, d6)
+
+
 @pytest.mark.parametrize("mode", [6, 7])
 def test_256cubed_stop_rule_bodies_exact_recomputed(queue, oracle, mode):
     """Modes 6 and 7 to tolerance: the same bodies and x as the dd oracle
