@@ -359,8 +359,9 @@ class CG:
         self.final_rxr = float("nan")  # extension: rxr after the last body
         self.poll_every = 32
         self.use_graph = True
-        self.mode = 0  # cgx_cg_set_mode: 0 auto (4 or 3), 1 three kernels, 2 fused, 3 deferred x,
-        # 4 fused + deferred x, 5 persistent body, 6 deferred x with Ap recomputed (lean walk)
+        self.mode = 0  # cgx_cg_set_mode: 0 auto (5, 4, 6 or 3), 1 three kernels, 2 fused,
+        # 3 deferred x, 4 fused + deferred x, 5 persistent body, 6 deferred x with Ap
+        # recomputed (lean walk), 7 fused + deferred x with Ap recomputed (tile walk)
 
     @classmethod
     def createCG(cls, dtype=np.float64, debug=Debuglevel.None_, device: int = 0) -> "CG":
