@@ -171,3 +171,9 @@ def test_g3_standin_solve_matches_oracle(queue, oracle, g3):
     assert rel(x, xr) <= 1e-6
     r = oracle.spmv(rp, cl, vl, x) - b
     assert np.linalg.norm(r) <= 10 * max(np.linalg.norm(oracle.spmv(rp, cl, vl, xr) - b), tol)
+    # and exactly the oracle's model of the engine's arithmetic (double-length
+    # dots): the same body count, the same x
+    xdd, rdd = oracle.cg_solve_dd(rp, cl, vl, b, tol, threads=16)
+    print("g3 dd oracle bodies", rdd.iterations)
+    assert rdd.stopped_by_tol and cg.iterations == rdd.iterations
+    assert np.array_equal(x, xdd), float(np.max(np.abs(x - xdd)))
