@@ -3,7 +3,8 @@
 * 512^3 on one GPU (134 M rows, the 8-GPU config's whole problem): the
   production SpMV format (value-code stencil SELL-P) equals the oracle's
   per-row loop and the general CSR-stream kernel bit for bit, five CG bodies
-  match the oracle's (OpenMP, 16 threads) at rel <= 1e-10, and the
+  match the oracle's (OpenMP, 16 threads) at rel <= 1e-10 and its
+  double-length-dot model (cg_solve_dd) bit for bit, and the
   deferred-x iteration (mode 3) equals the three-kernel one (mode 1) bit for
   bit over 12 bodies.
 * the G3_circuit stand-in at its real size (1,585,478 rows, irregular rows,
@@ -96,6 +97,11 @@ def test_512cubed_matches_oracle(queue, oracle):
     xr, res = oracle.cg_solve_omp(rp, cl, vl, b, 0.0, 16, max_iter=5)
     assert res.iterations == 5
     assert rel(xg, xr) <= 1e-10, rel(xg, xr)
+    del xr
+    # exactly the oracle's model of the engine's arithmetic (double-length
+    # dots), in the auto mode (4, the team form of the fused walk)
+    xdd, _ = oracle.cg_solve_dd(rp, cl, vl, b, 0.0, threads=16, max_iter=5)
+    assert np.array_equal(xg, xdd), float(np.max(np.abs(xg - xdd)))
 
 
 G3_N = 1_585_478
